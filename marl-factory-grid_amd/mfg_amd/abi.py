@@ -1,0 +1,103 @@
+"""ctypes mirror of include/mfg.h (the engine's C-ABI). Field order and sizes must match the header exactly;
+tests/test_abi.py checks sizeof() against the compiled libraries."""
+import ctypes as C
+
+MAX_AGENTS = 64
+MAX_ACTIONS = 16
+MAX_LAYERS = 32
+MAX_COMBINED = 72
+MAX_RULES = 32
+MAX_DOORS = 64
+
+# action opcodes
+ACT_NOOP, ACT_MOVE, ACT_CHARGE, ACT_CLEAN, ACT_DEST, ACT_DOORUSE, ACT_ITEM, ACT_MACHINE = range(8)
+# directions (North..NorthWest) and their (dx, dy) from utils/helpers.py:36-42
+DIR_NAMES = ['North', 'NorthEast', 'East', 'SouthEast', 'South', 'SouthWest', 'West', 'NorthWest']
+DIR_IDENT = ['north', 'north_east', 'east', 'south_east', 'south', 'south_west', 'west', 'north_west']
+DIR_DELTA = [(-1, 0), (-1, 1), (0, 1), (1, 1), (1, 0), (1, -1), (0, -1), (-1, -1)]
+
+# observation tags
+TAG_WALLS, TAG_DOORS, TAG_ITEMS, TAG_PODS, TAG_DROPOFFS, TAG_DIRT, TAG_DESTS, TAG_MACHINES, TAG_MAINTAINERS = range(9)
+TAG_AGENT0 = 16
+# layer kinds
+LAYER_ZERO, LAYER_TAG, LAYER_COMBINED, LAYER_BATTERY, LAYER_GLOBALPOS = range(5)
+
+# rule opcodes
+(RULE_SPAWN_BATTERIES, RULE_SPAWN_PODS, RULE_SPAWN_DROPOFFS, RULE_SPAWN_INVENTORIES, RULE_SPAWN_ITEMS,
+ RULE_SPAWN_DIRT, RULE_SPAWN_DESTS, RULE_SPAWN_MACHINES, RULE_SPAWN_MAINTAINERS, RULE_SPAWN_GLOBALPOS,
+ RULE_DOOR_AUTOCLOSE, RULE_RESPAWN_ITEMS, RULE_WATCH_COLLISIONS, RULE_BATTERY_DECHARGE, RULE_DONE_BATTERY,
+ RULE_DONE_MAXSTEPS, RULE_RESPAWN_DIRT, RULE_SMEAR_DIRT, RULE_DONE_DIRT, RULE_DEST_REACH, RULE_DONE_DEST,
+ RULE_MOVE_MAINTAINERS, RULE_DONE_MAINT_COLLISION) = range(1, 24)
+
+DEST_ANY, DEST_ALL, DEST_SIMULTANEOUS = range(3)
+
+
+class MfgAction(C.Structure):
+    _fields_ = [('op', C.c_int32), ('arg', C.c_int32), ('valid_reward', C.c_double), ('fail_reward', C.c_double),
+                ('aux0', C.c_double), ('aux1', C.c_double)]
+
+
+class MfgLayer(C.Structure):
+    _fields_ = [('kind', C.c_int32), ('tag', C.c_int32)]
+
+
+class MfgRule(C.Structure):
+    _fields_ = [('op', C.c_int32), ('i', C.c_int32 * 6), ('f', C.c_double * 6)]
+
+
+class MfgSpec(C.Structure):
+    _fields_ = [
+        ('abi_version', C.c_int32),
+        ('H', C.c_int32), ('W', C.c_int32),
+        ('level', C.POINTER(C.c_uint8)),
+        ('n_floor', C.c_int32), ('floor_cells', C.POINTER(C.c_int32)),
+        ('n_walls', C.c_int32), ('wall_cells', C.POINTER(C.c_int32)),
+        ('n_doors', C.c_int32), ('door_cells', C.POINTER(C.c_int32)),
+        ('door_closed_on_init', C.c_int32), ('door_auto_close', C.c_int32),
+        ('pomdp_r', C.c_int32),
+        ('n_rays', C.c_int32), ('ray_off', C.POINTER(C.c_int32)), ('ray_pts', C.POINTER(C.c_int32)),
+        ('n_agents', C.c_int32),
+        ('agent_blocking', C.c_int32 * MAX_AGENTS),
+        ('n_actions', C.c_int32 * MAX_AGENTS),
+        ('actions', (MfgAction * MAX_ACTIONS) * MAX_AGENTS),
+        ('n_layers', C.c_int32 * MAX_AGENTS),
+        ('layers', (MfgLayer * MAX_LAYERS) * MAX_AGENTS),
+        ('combined_n', C.c_int32 * MAX_AGENTS),
+        ('combined_tags', (C.c_int32 * MAX_COMBINED) * MAX_AGENTS),
+        ('has_batteries', C.c_int32), ('battery_initial', C.c_double),
+        ('has_inventories', C.c_int32),
+        ('has_items', C.c_int32),
+        ('items_quantity', C.c_int32),
+        ('has_pods', C.c_int32), ('pod_charge_rate', C.c_double),
+        ('has_dropoffs', C.c_int32),
+        ('has_dirt', C.c_int32),
+        ('dirt_quantity', C.c_int32),
+        ('dirt_initial_amount', C.c_double), ('dirt_clean_amount', C.c_double), ('dirt_max_global', C.c_double),
+        ('dirt_max_local', C.c_double), ('dirt_amount_var', C.c_double), ('dirt_n_var', C.c_double),
+        ('has_dests', C.c_int32), ('dest_action_counts', C.c_int32),
+        ('has_machines', C.c_int32), ('machine_work', C.c_int32), ('machine_pause', C.c_int32),
+        ('has_maintainers', C.c_int32),
+        ('has_globalpos', C.c_int32),
+        ('has_doors', C.c_int32),
+        ('n_rules', C.c_int32),
+        ('rules', MfgRule * MAX_RULES),
+        ('individual_rewards', C.c_int32),
+        ('env_seed', C.c_uint32),
+    ]
+
+
+class MfgEvents(C.Structure):
+    _fields_ = [
+        ('act', C.c_uint8 * MAX_AGENTS),
+        ('watch', C.c_uint8 * MAX_AGENTS),
+        ('door_coll', C.c_uint64),
+        ('maint_coll', C.c_uint64),
+        ('respawn_items_value', C.c_int32),
+        ('dirt_spawn_value', C.c_int32),
+        ('dirt_spawn_valid', C.c_int32),
+        ('dest_reach_agent', C.c_int32 * 4),
+        ('door_autoclose', C.c_int32),
+        ('done_mask', C.c_int32),
+        ('crashed', C.c_int32),
+        ('step', C.c_int32),
+    ]

@@ -1,0 +1,209 @@
+"""ctypes binding of the C oracle (oracle/mfg_oracle.c). TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() (as the checker) and bench.py's cpu_baseline leg.
+Build: `make -C oracle` (or __graft_entry__.build()) -> oracle/_build/liboracle.so.
+"""
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / '_build' / 'liboracle.so'
+
+CLS_NAMES = ['Wall', 'Door', 'Agent', 'Item', 'ChargePod', 'DropOffLocation', 'DirtPile', 'Destination',
+             'Machine', 'Maintainer']
+C_AGENT = 2
+
+
+class Res(C.Structure):
+    _fields_ = [('kind', C.c_int32), ('ent_kind', C.c_int32), ('ent', C.c_int32), ('ident', C.c_int32),
+                ('ident_arg', C.c_int32), ('valid', C.c_int32), ('collision', C.c_int32),
+                ('has_reward', C.c_int32), ('has_value', C.c_int32), ('aux', C.c_int32), ('reward', C.c_double),
+                ('value', C.c_double)]
+
+
+def build(force=False):
+    src = HERE / 'mfg_oracle.c'
+    if force or not LIB.exists() or LIB.stat().st_mtime < max(src.stat().st_mtime,
+                                                              (HERE.parent / 'include' / 'mfg.h').stat().st_mtime):
+        LIB.parent.mkdir(exist_ok=True)
+        subprocess.check_call(['gcc', '-O2', '-shared', '-fPIC', '-o', str(LIB), str(src), '-lm'])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(str(LIB))
+        L.oracle_create.restype = C.c_void_p
+        L.oracle_create.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.oracle_destroy.argtypes = [C.c_void_p]
+        L.oracle_reset.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_step.argtypes = [C.c_void_p] * 6
+        for fn in ('oracle_results', 'oracle_header', 'oracle_entities', 'oracle_group', 'oracle_agents',
+                   'oracle_doors', 'oracle_posdict', 'oracle_floor', 'oracle_keyrank', 'oracle_mt', 'oracle_pcg'):
+            getattr(L, fn).restype = C.c_int
+        L.oracle_results.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.oracle_header.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_entities.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_group.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_agents.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_doors.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_posdict.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        for fn in ('oracle_floor', 'oracle_keyrank', 'oracle_mt', 'oracle_pcg'):
+            getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_mt_u32_seq.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_mt_shuffle_range.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_pcg_seq.argtypes = [C.c_uint32, C.c_int, C.c_void_p, C.c_void_p, C.c_double, C.c_double]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class OracleEnv:
+    """One reference environment restated in C (single env, exact)."""
+
+    def __init__(self, spec, py_seed):
+        from mfg_amd.spec import seed_key
+        from mfg_amd import abi
+        self.spec = spec
+        self.L = lib()
+        key = seed_key(py_seed)
+        self._key = key
+        self.h = self.L.oracle_create(C.byref(spec.c), _p(key), len(key))
+        self.A = spec.n_agents
+        self.d = spec.d
+        self._obs = np.zeros((self.A, abi.MAX_LAYERS, self.d, self.d), np.float64)
+        self._rew = np.zeros(self.A, np.float64)
+        self._done = np.zeros(1, np.uint8)
+        self.ev = abi.MfgEvents()
+
+    def close(self):
+        if self.h:
+            self.L.oracle_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def obs_list(self):
+        return [self._obs[a, :n].copy() for a, n in enumerate(self.spec.n_layers)]
+
+    def reset(self):
+        self.L.oracle_reset(self.h, _p(self._obs))
+        return self.obs_list()
+
+    def step(self, actions, with_obs=True):
+        act = np.ascontiguousarray(actions, np.int32)
+        self.L.oracle_step(self.h, _p(act), _p(self._rew), _p(self._done),
+                           _p(self._obs) if with_obs else None, C.addressof(self.ev))
+        return self._rew.copy(), bool(self._done[0]), self.ev
+
+    # ---- inspection ----
+    def header(self):
+        out = np.zeros(64, np.int32)
+        n = self.L.oracle_header(self.h, _p(out))
+        return out[:n]
+
+    def entities(self):
+        nE = int(self.header()[3])
+        ent = np.zeros((nE, 5), np.int32)
+        amt = np.zeros(nE, np.float64)
+        self.L.oracle_entities(self.h, _p(ent), _p(amt))
+        return ent, amt
+
+    def ent_name(self, ent, h):
+        cls, i = int(ent[h, 0]), int(ent[h, 1])
+        if cls == C_AGENT:
+            return f'Agent[{self.spec.agent_names[i]}]'
+        return f'{CLS_NAMES[cls]}[{i}]'
+
+    def group(self, which):
+        out = np.zeros(100000, np.int32)
+        n = self.L.oracle_group(self.h, which, _p(out))
+        return out[:n]
+
+    def agents(self):
+        pos = np.zeros(self.A, np.int32)
+        bat = np.zeros(self.A, np.float64)
+        st = np.zeros(2 * self.A, np.int32)
+        self.L.oracle_agents(self.h, _p(pos), _p(bat), _p(st))
+        return pos, bat, st.reshape(-1, 2)
+
+    def doors(self):
+        n = self.spec.c.n_doors
+        o = np.zeros(max(n, 1), np.int32)
+        t = np.zeros(max(n, 1), np.int32)
+        self.L.oracle_doors(self.h, _p(o), _p(t))
+        return o[:n], t[:n]
+
+    def posdict(self, skip_walls=True):
+        buf = np.zeros(1 << 20, np.int32)
+        n = self.L.oracle_posdict(self.h, _p(buf), len(buf))
+        ent, _ = self.entities()
+        out, k = {}, 0
+        while k < n:
+            cell, m = int(buf[k]), int(buf[k + 1])
+            hs = buf[k + 2:k + 2 + m]
+            k += 2 + m
+            names = [self.ent_name(ent, int(h)) for h in hs]
+            if skip_walls and all(x.startswith('Wall[') for x in names):
+                continue
+            out[cell] = names
+        return out
+
+    def floor(self):
+        out = np.zeros(self.spec.c.n_floor, np.int32)
+        self.L.oracle_floor(self.h, _p(out))
+        return out
+
+    def keyrank(self):
+        out = np.zeros(self.spec.H * self.spec.W, np.int32)
+        self.L.oracle_keyrank(self.h, _p(out))
+        return out
+
+    def mt_state(self):
+        out = np.zeros(625, np.uint32)
+        self.L.oracle_mt(self.h, _p(out))
+        return out
+
+    def pcg_state(self):
+        out = np.zeros(4, np.uint64)
+        self.L.oracle_pcg(self.h, _p(out))
+        return out
+
+    def results(self):
+        buf = (Res * 4096)()
+        n = self.L.oracle_results(self.h, buf, 4096)
+        return list(buf[:n])
+
+
+def mt_u32_seq(key, n):
+    out = np.zeros(n, np.uint32)
+    key = np.ascontiguousarray(key, np.uint32)
+    lib().oracle_mt_u32_seq(_p(key), len(key), n, _p(out))
+    return out
+
+
+def mt_shuffle_range(key, n):
+    out = np.zeros(n, np.int32)
+    nxt = np.zeros(1, np.uint32)
+    key = np.ascontiguousarray(key, np.uint32)
+    lib().oracle_mt_shuffle_range(_p(key), len(key), n, _p(out), _p(nxt))
+    return out, int(nxt[0])
+
+
+def pcg_seq(seed, n, lo, hi):
+    raw = np.zeros(n, np.uint64)
+    uni = np.zeros(n, np.float64)
+    lib().oracle_pcg_seq(seed, n, _p(raw), _p(uni), lo, hi)
+    return raw, uni

@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Golden-fixture generator: runs the REFERENCE marl-factory-grid (imported read-only from /root/reference
+through the minimal stand-ins in tools/standins/) and records per-step snapshots for parity tests.
+
+THIS SCRIPT RUNS ONLY IN THE DEVELOPMENT CONTAINER (it needs /root/reference). It is never imported by the
+product, by bench.py, or on the GPU box. Its outputs are small data fixtures under tests/golden/.
+
+Seeding contract: `random.seed(py_seed)` then `Object._u_idx.clear()` then `Factory(cfg)`;
+`General.env_seed` seeds numpy's PCG64 inside the reference (utils/states.py:114).
+Actions come from numpy.random.default_rng(action_seed) (a separate stream: the reference's own global
+`random` must not be touched by the harness) and are stored verbatim in the fixture.
+"""
+import argparse
+import contextlib
+import gzip
+import hashlib
+import io
+import json
+import os
+import random
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(REPO / 'tools' / 'standins'), '/root/reference']
+
+from marl_factory_grid.environment.entity.object import Object  # noqa: E402
+from marl_factory_grid.environment.factory import Factory  # noqa: E402
+from marl_factory_grid.utils.ray_caster import RayCaster  # noqa: E402
+
+CFG_DIR = REPO / 'marl-factory-grid_amd' / 'mfg_amd' / 'configs'
+LVL_DIR = REPO / 'marl-factory-grid_amd' / 'mfg_amd' / 'levels'
+
+
+def _group(env, name):
+    # never env[name]: a missing group inserts None into Entities._data
+    return env.state.entities._data.get(name)
+
+
+def _h(b: bytes) -> str:
+    return hashlib.sha1(b).hexdigest()[:16]
+
+
+def mt_digest():
+    st = random.getstate()[1]
+    return _h(np.asarray(st, dtype=np.uint32).tobytes())
+
+
+def floor_arr(env, W):
+    fl = env.state.entities._floor_positions
+    return np.asarray([x * W + y for x, y in fl], dtype=np.int32)
+
+
+def posdict_dump(env, W, skip_walls=True):
+    """cell -> list of entity names, in pos_dict insertion order; only non-empty in-grid cells."""
+    out = {}
+    for pos, ents in env.state.entities.pos_dict.items():
+        if not ents:
+            continue
+        names = [e.name for e in ents]
+        if skip_walls and all(n.startswith('Wall[') for n in names):
+            continue
+        out[int(pos[0]) * W + int(pos[1])] = names
+    return dict(sorted(out.items()))
+
+
+def posdict_sha(pd):
+    return _h(json.dumps(sorted((int(k), v) for k, v in pd.items())).encode())
+
+
+def snapshot(env, W):
+    s = {}
+    ag = _group(env, 'Agent')
+    s['agent_pos'] = [list(map(int, a.pos)) for a in ag]
+    s['agent_state'] = [[str(a.state.identifier), bool(a.state.validity)] for a in ag]
+    for gname, key in [('Doors', 'doors'), ('Items', 'items'), ('ChargePods', 'pods'),
+                       ('DropOffLocations', 'dropoffs'), ('Destinations', 'dests'), ('DirtPiles', 'dirt'),
+                       ('Machines', 'machines'), ('Maintainers', 'maintainers')]:
+        g = _group(env, gname)
+        if g is None:
+            continue
+        rows = []
+        for e in g:
+            r = [int(e.u_int), int(e.pos[0]), int(e.pos[1])]
+            if gname == 'Doors':
+                r += [int(e.is_open), int(e.time_to_close)]
+            elif gname == 'DirtPiles':
+                r += [float(e.amount)]
+            elif gname == 'Destinations':
+                r += [int(e.was_reached())]
+            elif gname == 'Machines':
+                r += [int(e.health), str(e.status)]
+            rows.append(r)
+        s[key] = rows
+    b = _group(env, 'Batteries')
+    if b is not None:
+        s['battery'] = [float(x.charge_level) for x in b]
+    s['u_idx'] = dict(Object._u_idx)
+    s['mt'] = mt_digest()
+    s['pcg'] = str(env.state.rng.bit_generator.state['state']['state'])
+    return s
+
+
+def run(cfg_name, py_seed, n_steps, action_seed, full_obs_every, level_path=None):
+    cfg = CFG_DIR / cfg_name
+    random.seed(py_seed)
+    Object._u_idx.clear()
+    sink = io.StringIO()
+    with contextlib.redirect_stdout(sink):
+        env = Factory(str(cfg), custom_level_path=level_path)
+        obs = env.reset()
+    H, W = env.map.level_shape
+    arng = np.random.default_rng(action_seed)
+    n_act = [len(a.actions) for a in _group(env, 'Agent')]
+    rec = dict(config=cfg_name, py_seed=py_seed, action_seed=action_seed, H=H, W=W,
+               agent_names=[a.name for a in _group(env, 'Agent')], n_actions=n_act,
+               named_action_space=env.named_action_space,
+               obs_layers={k: list(v) for k, v in env.obs_builder.obs_layers.items()},
+               steps=[])
+    obs_full = {}
+    floor_at_reset = {}
+    keyorder_at_reset = {}
+
+    def cell_keys():
+        return [int(p[0]) * W + int(p[1]) for p in env.state.entities.pos_dict.keys()
+                if 0 <= p[0] < H and 0 <= p[1] < W]
+
+    def record(t_global, episode, step, actions, reward, done, info, obs_list, crashed=None):
+        o = np.stack([np.asarray(x, dtype=np.float64) for x in obs_list]) if obs_list else np.zeros(0)
+        pd = posdict_dump(env, W)
+        ent = dict(t=t_global, episode=episode, step=step, actions=actions,
+                   reward=reward, done=done, info=info, obs_sha=_h(o.tobytes()),
+                   floor_sha=_h(floor_arr(env, W).tobytes()), posdict_sha=posdict_sha(pd))
+        if step <= 3 or t_global % full_obs_every == 0:
+            ent['posdict'] = pd
+        if crashed:
+            ent['crashed'] = crashed
+        ent.update(snapshot(env, W))
+        rec['steps'].append(ent)
+        if step <= 3 or t_global % full_obs_every == 0:
+            obs_full[f't{t_global}'] = o
+
+    episode, step = 0, 0
+    floor_at_reset['e0'] = floor_arr(env, W)
+    keyorder_at_reset['e0'] = np.asarray(cell_keys(), dtype=np.int32)
+    record(0, 0, 0, None, None, False, None, list(obs.values()))
+    t = 0
+    while t < n_steps:
+        t += 1
+        step += 1
+        acts = [int(arng.integers(0, n)) for n in n_act]
+        crashed = None
+        with contextlib.redirect_stdout(sink):
+            try:
+                _, o, r, d, info = env.step(acts)
+            except Exception as ex:  # reference crash paths: record and end the episode
+                crashed = f'{type(ex).__name__}: {ex}'
+                o, r, d, info = [], None, True, None
+        info = None if info is None else {k: float(v) for k, v in info.items()}
+        record(t, episode, step, acts, None if r is None else [float(x) for x in r], bool(d), info, o, crashed)
+        if d:
+            episode += 1
+            step = 0
+            with contextlib.redirect_stdout(sink):
+                obs = env.reset()
+            floor_at_reset[f'e{episode}'] = floor_arr(env, W)
+            keyorder_at_reset[f'e{episode}'] = np.asarray(cell_keys(), dtype=np.int32)
+            record(t, episode, 0, None, None, False, None, list(obs.values()))
+    return rec, obs_full, floor_at_reset, keyorder_at_reset
+
+
+def unit_vectors(out):
+    """RNG + ray-table known answers from the libraries/reference the restatements follow."""
+    vec = {}
+    random.seed(12345)
+    vec['mt_seed12345_first2000'] = np.asarray([random.getrandbits(32) for _ in range(2000)], dtype=np.uint32)
+    for seed in (0, 1, 7, 2**40 + 3):
+        for n in (2, 95, 120, 1077):
+            random.seed(seed)
+            x = list(range(n))
+            random.shuffle(x)
+            vec[f'shuffle_s{seed}_n{n}'] = np.asarray(x, dtype=np.int32)
+            vec[f'shuffle_s{seed}_n{n}_next'] = np.asarray([random.getrandbits(32)], dtype=np.uint32)
+    rng = np.random.default_rng(69)
+    vec['pcg69_uniform'] = np.asarray([rng.uniform(-0.2, 0.2) for _ in range(64)], dtype=np.float64)
+    vec['pcg69_raw'] = np.random.default_rng(69).bit_generator.random_raw(16).astype(np.uint64)
+    for r in (3, 4, 8):
+        d = 2 * r + 1
+
+        class _A:
+            pos = (0, 0)
+            name = 'probe'
+        rc = RayCaster(_A(), d)
+        rays = rc.get_rays()
+        flat, lens = [], []
+        for ray in rays:
+            lens.append(len(ray))
+            flat.extend([p for pt in ray for p in pt])
+        vec[f'rays_r{r}_len'] = np.asarray(lens, dtype=np.int32)
+        vec[f'rays_r{r}_pts'] = np.asarray(flat, dtype=np.int32)
+    np.savez_compressed(out, **vec)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='large8.yaml')
+    ap.add_argument('--seeds', default='0,1')
+    ap.add_argument('--steps', type=int, default=1200)
+    ap.add_argument('--full-obs-every', type=int, default=97)
+    ap.add_argument('--tag', default=None)
+    ap.add_argument('--units', action='store_true')
+    args = ap.parse_args()
+    outdir = REPO / 'tests' / 'golden'
+    outdir.mkdir(parents=True, exist_ok=True)
+    if args.units:
+        unit_vectors(outdir / 'units.npz')
+        print('wrote units.npz')
+        return
+    level_path = None
+    tag = args.tag or Path(args.config).stem
+    for s in [int(x) for x in args.seeds.split(',')]:
+        rec, obs_full, floors, keys = run(args.config, s, args.steps, 1000 + s, args.full_obs_every, level_path)
+        base = outdir / f'{tag}_s{s}'
+        with gzip.open(f'{base}.json.gz', 'wt') as f:
+            json.dump(rec, f, separators=(',', ':'))
+        np.savez_compressed(f'{base}.npz', **obs_full,
+                            **{f'floor_{k}': v for k, v in floors.items()},
+                            **{f'keys_{k}': v for k, v in keys.items()})
+        print(f'wrote {base}.json/.npz: {len(rec["steps"])} records, {os.path.getsize(f"{base}.json.gz")} B json.gz')
+
+
+if __name__ == '__main__':
+    main()
