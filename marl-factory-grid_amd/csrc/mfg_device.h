@@ -1,0 +1,78 @@
+// mfg_device.h — device-side data structures of the MI355X batched step engine.
+//
+// Execution model: ONE WAVEFRONT PER ENVIRONMENT. A 64-lane wave owns one env for a whole launch:
+//  * per-env entity tables are lane-distributed (lane i holds entity slot i of each group);
+//  * the sequential parts of the reference step (agents act in list order, states.py:187-196) run as
+//    wave-uniform control flow; set queries ("is there an X at cell c") are wave ballots;
+//  * the RNG streams (MT19937 + floor-list permutation) live in the wave's LDS slice, the MT twist is
+//    lane-parallel, rejection sampling for random.shuffle is resolved 64 draws at a time with ballots,
+//    only the Fisher-Yates swap chain itself is serial;
+//  * the observation render maps lanes to rays (walk) and then to window cells (placement), so obs
+//    stores are coalesced runs of d*d values per layer.
+// The env state lives in HBM as one contiguous record per env (layout below), so a wave's loads and
+// stores of its env are contiguous/coalesced.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mfg.h"
+
+#define MFG_WAVE 64
+#define MFG_HDR_N 32
+
+// header slots (int32) of the per-env record
+enum {
+  H_STEP = 0,      // Gamestate.curr_step
+  H_EPISODE,       // number of resets done
+  H_CRASHED,       // reference crash path hit
+  H_FROZEN,        // episode-1 agent objects replaced (Q11/Q12)
+  H_OBS_INIT,      // OBSBuilder has built once (ray casters exist)
+  H_DEBT,          // pending floor-list shuffles (replayed before any order-dependent consumer)
+  H_MT_IDX,        // MT19937 index
+  H_N_ITEMS, H_N_PODS, H_N_DROPS, H_N_DIRT, H_N_DESTS,
+  H_ITEM_BASE, H_POD_BASE, H_DROP_BASE, H_DEST_BASE, H_BAT_BASE,
+  H_ARRIVAL,       // Agents-group insertion counter (arrival order per cell)
+  H_DONE,          // last step's done flag (auto-reset bookkeeping)
+  H_OVERFLOW,      // capacity overflow (dirt piles > MFG_DIRT_MAX etc.) -> env flagged
+  H_CNT_AGENT, H_CNT_BATTERY, H_CNT_POD, H_CNT_DROP, H_CNT_ITEM, H_CNT_DIRT, H_CNT_DEST, H_CNT_MACHINE,
+  H_CNT_MAINT, H_CNT_GP,
+  H_TOTAL_STEPS,   // env-steps since creation (Philox counter)
+  H__END
+};
+static_assert(H__END <= MFG_HDR_N, "header overflow");
+
+#define MFG_DIRT_MAX 64
+
+// packed entity words (int32): pos in bits 0..15 (0xFFFF = VALUE_NO_POS), flags above
+#define EW_POS(w) ((w) & 0xFFFF)
+#define EW_ALIVE 0x10000     // member of its collection (Collection._data)
+#define EW_PRESENT 0x20000   // present in the global pos_dict (identifier-dedup may keep it out, Q14)
+#define EW_REACHED 0x40000   // destination reached
+#define EW_NOPOS 0xFFFF
+// door word: bit0 open, bits 8..15 time_to_close, bit16 present in the global pos_dict
+#define DW_OPEN 1
+#define DW_TTC(w) (((w) >> 8) & 0xFF)
+#define DW_PRESENT 0x10000
+
+struct MfgLayout {
+  int32_t size;  // bytes per env record (multiple of 16)
+  int32_t o_hdr, o_rule_ctr, o_agent_pos, o_agent_arr, o_agent_par, o_frozen_org, o_frozen_gp;
+  int32_t o_door, o_items, o_pods, o_drops, o_dests, o_dirt_pos, o_dirt_id;
+  int32_t o_battery, o_frozen_bat, o_dirt_amt, o_pcg, o_mt, o_perm;
+};
+
+struct MfgDevSpec {
+  mfg_spec s;  // table pointers inside are HOST pointers: never dereferenced on the device
+  int32_t HW, nf, nw, nd, A, r, d, dd, nrays, maxpts, lmax;
+  int32_t imax, pmax, dropmax, destmax;
+  int32_t obs_agent_stride;  // lmax*dd
+  const uint8_t* level;      // [HW] 0 floor 1 wall 2 door
+  const uint8_t* door_of;    // [HW] door index or 0xFF
+  const int32_t* wall_cells; // [nw]
+  const int32_t* door_cells; // [nd]
+  const int32_t* floor_init; // [nf]
+  const int8_t* ray_pts;     // [nrays][maxpts][2] (dx, dy), padded
+  const uint8_t* ray_len;    // [nrays]
+  uint64_t pcg_init_hi, pcg_init_lo, pcg_inc_hi, pcg_inc_lo;  // default_rng(env_seed) state after seeding
+  MfgLayout L;
+  int32_t lds_per_wave;      // bytes of dynamic LDS per wave
+};

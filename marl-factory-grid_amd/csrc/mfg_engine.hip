@@ -1,0 +1,1599 @@
+// mfg_engine.hip — MI355X (gfx950) batched step engine for the marl-factory-grid world.
+//
+// Replaces, for a batch of B independent environments:
+//   Factory.reset / Factory.step       marl_factory_grid/environment/factory.py:134-148, 189-259
+//   Gamestate.tick / check_done        marl_factory_grid/utils/states.py:170-226
+//   rule hooks + actions of the modules listed in mfg.h
+//   OBSBuilder.build_for_all           marl_factory_grid/utils/observation_builder.py:96-235
+// bit-exactly, including the reference's RNG streams (CPython MT19937 floor shuffles, numpy PCG64
+// uniform draws) and its documented quirks.
+//
+// See mfg_device.h for the execution model (one wavefront per env).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "mfg_device.h"
+
+typedef unsigned long long u64;
+
+// ------------------------------------------------------------------------------------------------
+// wave primitives
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+__device__ __forceinline__ u64 ballot(bool p) { return (u64)__ballot(p); }
+__device__ __forceinline__ int popc(u64 m) { return __popcll(m); }
+__device__ __forceinline__ u64 lt_mask() { return (1ull << lane_id()) - 1ull; }
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
+__device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ u64 wave_or64(u64 v) {
+  unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo |= __shfl_xor(lo, o);
+    hi |= __shfl_xor(hi, o);
+  }
+  return ((u64)hi << 32) | lo;
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-wave env context: the env record is mirrored 1:1 in the wave's LDS slice
+// ------------------------------------------------------------------------------------------------
+struct Env {
+  const MfgDevSpec* S;
+  uint8_t* lds;  // this wave's LDS slice == image of the HBM record
+  int lane;
+  __device__ int* hdr() const { return (int*)(lds + S->L.o_hdr); }
+  __device__ int* rctr() const { return (int*)(lds + S->L.o_rule_ctr); }
+  __device__ int* agpos() const { return (int*)(lds + S->L.o_agent_pos); }
+  __device__ int* agarr() const { return (int*)(lds + S->L.o_agent_arr); }
+  __device__ int* agpar() const { return (int*)(lds + S->L.o_agent_par); }
+  __device__ int* forg() const { return (int*)(lds + S->L.o_frozen_org); }
+  __device__ int* fgp() const { return (int*)(lds + S->L.o_frozen_gp); }
+  __device__ int* door() const { return (int*)(lds + S->L.o_door); }
+  __device__ int* items() const { return (int*)(lds + S->L.o_items); }
+  __device__ int* pods() const { return (int*)(lds + S->L.o_pods); }
+  __device__ int* drops() const { return (int*)(lds + S->L.o_drops); }
+  __device__ int* dests() const { return (int*)(lds + S->L.o_dests); }
+  __device__ int* dirtpos() const { return (int*)(lds + S->L.o_dirt_pos); }
+  __device__ int* dirtid() const { return (int*)(lds + S->L.o_dirt_id); }
+  __device__ double* bat() const { return (double*)(lds + S->L.o_battery); }
+  __device__ double* fbat() const { return (double*)(lds + S->L.o_frozen_bat); }
+  __device__ double* dirtamt() const { return (double*)(lds + S->L.o_dirt_amt); }
+  __device__ uint64_t* pcg() const { return (uint64_t*)(lds + S->L.o_pcg); }
+  __device__ uint32_t* mt() const { return (uint32_t*)(lds + S->L.o_mt); }
+  __device__ uint16_t* perm() const { return (uint16_t*)(lds + S->L.o_perm); }
+  // uniform header access
+  __device__ int H(int k) const { return uni(hdr()[k]); }
+  __device__ void setH(int k, int v) const {
+    if (lane == 0) hdr()[k] = v;
+  }
+};
+
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// copy record HBM <-> LDS (16 B per lane per iteration, coalesced)
+__device__ void rec_load(const Env& e, const uint8_t* g) {
+  const int n16 = e.S->L.size >> 4;
+  const uint4* src = (const uint4*)g;
+  uint4* dst = (uint4*)e.lds;
+  for (int i = e.lane; i < n16; i += MFG_WAVE) dst[i] = src[i];
+  wave_sync();
+}
+__device__ void rec_store(const Env& e, uint8_t* g) {
+  wave_sync();
+  const int n16 = e.S->L.size >> 4;
+  const uint4* src = (const uint4*)e.lds;
+  uint4* dst = (uint4*)g;
+  for (int i = e.lane; i < n16; i += MFG_WAVE) dst[i] = src[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// MT19937 (CPython semantics) — state in LDS, lane-parallel twist
+// ------------------------------------------------------------------------------------------------
+#define MT_UPPER 0x80000000u
+#define MT_LOWER 0x7fffffffu
+#define MT_MATRIX 0x9908b0dfu
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
+  return c ^ (y >> 1) ^ ((y & 1u) ? MT_MATRIX : 0u);
+}
+// In-place twist in three dependency phases; within a wave every LDS read of an iteration is issued
+// before its writes, and later iterations only read indices no earlier iteration has written.
+__device__ void mt_twist(const Env& e) {
+  uint32_t* mt = e.mt();
+  const int lane = e.lane;
+  for (int b = 0; b < 227; b += MFG_WAVE) {
+    int i = b + lane;
+    uint32_t v = 0;
+    if (i < 227) v = mt_mix(mt[i], mt[i + 1], mt[i + 397]);
+    wave_sync();
+    if (i < 227) mt[i] = v;
+    wave_sync();
+  }
+  for (int b = 227; b < 623; b += MFG_WAVE) {
+    int i = b + lane;
+    uint32_t v = 0;
+    if (i < 623) v = mt_mix(mt[i], mt[i + 1], mt[i - 227]);
+    wave_sync();
+    if (i < 623) mt[i] = v;
+    wave_sync();
+  }
+  if (lane == 0) mt[623] = mt_mix(mt[623], mt[0], mt[396]);
+  wave_sync();
+}
+
+// Draw random.randbelow(i+1) for i = hi, hi-1, ..., lo (the inner loop of random.shuffle,
+// random.py:380-395 with _randbelow_with_getrandbits, random.py:239-249). 64 draws are tempered in
+// parallel; which draws are accepted (and for which i) is the fixed point of
+//   A_l = #accepted lanes < l,  i_l = icur - A_l,  accept_l = (y_l >> (32 - bitlen(i_l+1))) <= i_l,
+// found by Jacobi iteration with ballots (lane 0 is exact after 1 round, lane l after l+1; typical 2-3).
+// If perm != null the Fisher-Yates swaps are applied in order (the only serial part).
+// Returns j of the first accepted draw (i == hi), used by empty_positions().pop().
+__device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
+  uint32_t* mt = e.mt();
+  const int lane = e.lane;
+  int idx = e.H(H_MT_IDX);
+  int icur = hi;
+  int first_j = -1;
+  while (icur >= lo) {
+    if (idx >= 624) {
+      mt_twist(e);
+      idx = 0;
+    }
+    const int lmax = 624 - idx;
+    const bool has = lane < lmax;
+    const uint32_t y = has ? mt_temper(mt[idx + lane]) : 0u;
+    int A = lane;
+    u64 accm;
+    int il;
+    uint32_t r;
+    bool act, acc;
+    for (;;) {
+      il = icur - A;
+      act = has && il >= lo;
+      uint32_t n = act ? (uint32_t)(il + 1) : 2u;
+      int k = 32 - __clz((int)n);
+      r = act ? (y >> (32 - k)) : 0u;
+      acc = act && r <= (uint32_t)il;
+      accm = ballot(acc);
+      int An = popc(accm & lt_mask());
+      if (!ballot(An != A)) break;
+      A = An;
+    }
+    const int consumed = popc(ballot(act));
+    const int nacc = popc(accm);
+    if (first_j < 0 && nacc) first_j = rl((int)r, ffs64(accm));
+    if (perm) {
+      // serial Fisher-Yates swaps for the accepted draws, in draw order
+      const int ri = (int)r;
+      if (lane == 0) {
+        u64 m = accm;
+        while (m) {
+          const int L = ffs64(m);
+          m &= m - 1;
+          const int i = rl(il, L), j = rl(ri, L);
+          const uint16_t a = perm[i], b = perm[j];
+          perm[i] = b;
+          perm[j] = a;
+        }
+      }
+      wave_sync();
+    }
+    icur -= nacc;
+    idx += consumed;
+  }
+  e.setH(H_MT_IDX, idx);
+  wave_sync();
+  return first_j;
+}
+
+// random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
+__device__ __forceinline__ void floor_shuffle(const Env& e) { mt_randbelow_seq(e, e.S->nf - 1, 1, e.perm()); }
+
+// Pay the shuffle debt accumulated by membership-only floorlist calls (check_pos_validity, Q3).
+__device__ void pay_debt(const Env& e) {
+  int debt = e.H(H_DEBT);
+  for (int k = 0; k < debt; k++) floor_shuffle(e);
+  e.setH(H_DEBT, 0);
+  wave_sync();
+}
+
+// CPython random.seed(int) -> init_by_array (Modules/_randommodule.c); serial, once per env
+__device__ void mt_seed(const Env& e, const uint32_t* key, int len) {
+  uint32_t* mt = e.mt();
+  if (e.lane == 0) {
+    mt[0] = 19650218u;
+    for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    int i = 1, j = 0;
+    int k = 624 > len ? 624 : len;
+    for (; k; k--) {
+      mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+      i++; j++;
+      if (i >= 624) { mt[0] = mt[623]; i = 1; }
+      if (j >= len) j = 0;
+    }
+    for (k = 623; k; k--) {
+      mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+      i++;
+      if (i >= 624) { mt[0] = mt[623]; i = 1; }
+    }
+    mt[0] = 0x80000000u;
+  }
+  e.setH(H_MT_IDX, 624);
+  wave_sync();
+}
+
+// ------------------------------------------------------------------------------------------------
+// numpy PCG64 (XSL-RR 128/64) + Generator.uniform — state in LDS (4 x u64: state hi, lo, inc hi, lo)
+// ------------------------------------------------------------------------------------------------
+__device__ double pcg_uniform(const Env& e, double lo, double hi) {
+  uint64_t* p = e.pcg();
+  unsigned __int128 st = ((unsigned __int128)p[0] << 64) | p[1];
+  const unsigned __int128 inc = ((unsigned __int128)p[2] << 64) | p[3];
+  const unsigned __int128 mult = ((unsigned __int128)2549297995355413924ULL << 64) | 4865540595714422341ULL;
+  st = st * mult + inc;
+  const uint64_t h = (uint64_t)(st >> 64), l = (uint64_t)st;
+  const unsigned rot = (unsigned)(h >> 58);
+  const uint64_t x = h ^ l;
+  const uint64_t out = (x >> rot) | (x << ((64 - rot) & 63));
+  wave_sync();
+  if (e.lane == 0) { p[0] = (uint64_t)(st >> 64); p[1] = (uint64_t)st; }
+  wave_sync();
+  const double u = (double)(out >> 11) * (1.0 / 9007199254740992.0);
+  return lo + (hi - lo) * u;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (synthetic actions for fused rollouts): key (seed, env), counter (step, agent, 0, 0)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t philox_u32(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1) {
+  uint32_t c2 = 0, c3 = 0;
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// entity model queries (global pos_dict semantics, groups/objects.py:193-214)
+// ------------------------------------------------------------------------------------------------
+enum { K_NONE = -1, K_DOOR = 1, K_ITEM = 3, K_POD = 4, K_DROP = 5, K_DIRT = 6, K_DEST = 7 };
+
+// ballot of group slots at `cell` whose word has all bits of `need`
+__device__ __forceinline__ u64 grp_at(const int* tbl, int n, int cell, int need, int lane) {
+  int w = lane < n ? tbl[lane] : 0;
+  return ballot(lane < n && EW_POS(w) == cell && (w & need) == need);
+}
+__device__ __forceinline__ u64 agents_at(const Env& e, int cell) {
+  const int A = e.S->A;
+  int p = e.lane < A ? e.agpos()[e.lane] : -1;
+  return ballot(e.lane < A && p == cell);
+}
+__device__ __forceinline__ int door_idx(const Env& e, int cell) {
+  int d = e.S->door_of[cell];
+  return d == 0xFF ? -1 : d;
+}
+// the present int-identifier entity at `cell` whose identifier equals `id` (at most one, pos_dict keeps
+// identifiers unique per cell); returns its kind, *slot = group slot
+__device__ int find_present_id(const Env& e, int cell, int id, int* slot) {
+  const int lane = e.lane;
+  int d = door_idx(e, cell);
+  if (d >= 0 && d == id && (e.door()[d] & DW_PRESENT)) { *slot = d; return K_DOOR; }
+  u64 m;
+  int base = e.H(H_ITEM_BASE);
+  m = grp_at(e.items(), e.H(H_N_ITEMS), cell, EW_PRESENT, lane) & ballot(base + lane == id);
+  if (m) { *slot = ffs64(m); return K_ITEM; }
+  base = e.H(H_POD_BASE);
+  m = grp_at(e.pods(), e.H(H_N_PODS), cell, EW_PRESENT, lane) & ballot(base + lane == id);
+  if (m) { *slot = ffs64(m); return K_POD; }
+  base = e.H(H_DROP_BASE);
+  m = grp_at(e.drops(), e.H(H_N_DROPS), cell, EW_PRESENT, lane) & ballot(base + lane == id);
+  if (m) { *slot = ffs64(m); return K_DROP; }
+  base = e.H(H_DEST_BASE);
+  m = grp_at(e.dests(), e.H(H_N_DESTS), cell, EW_PRESENT, lane) & ballot(base + lane == id);
+  if (m) { *slot = ffs64(m); return K_DEST; }
+  const int nd = e.H(H_N_DIRT);
+  m = grp_at(e.dirtpos(), nd, cell, EW_PRESENT, lane) & ballot(lane < nd && e.dirtid()[lane < nd ? lane : 0] == id);
+  if (m) { *slot = ffs64(m); return K_DIRT; }
+  return K_NONE;
+}
+// Objects.notify_del_entity x2 on the global pos_dict: list.remove() drops the first identifier-equal entry
+__device__ void global_remove_id(const Env& e, int cell, int id) {
+  int slot;
+  int k = find_present_id(e, cell, id, &slot);
+  if (e.lane == 0) {
+    switch (k) {
+      case K_DOOR: e.door()[slot] &= ~DW_PRESENT; break;
+      case K_ITEM: e.items()[slot] &= ~EW_PRESENT; break;
+      case K_POD: e.pods()[slot] &= ~EW_PRESENT; break;
+      case K_DROP: e.drops()[slot] &= ~EW_PRESENT; break;
+      case K_DEST: e.dests()[slot] &= ~EW_PRESENT; break;
+      case K_DIRT: e.dirtpos()[slot] &= ~EW_PRESENT; break;
+      default: break;
+    }
+  }
+  wave_sync();
+}
+__device__ __forceinline__ bool present_closed_door(const Env& e, int cell) {
+  int d = door_idx(e, cell);
+  if (d < 0) return false;
+  int w = e.door()[d];
+  return (w & DW_PRESENT) && !(w & DW_OPEN);
+}
+// any entity blocking the position (states.py:259-270): walls, closed doors, blocking agents
+__device__ bool blocked_at(const Env& e, int cell) {
+  if (e.S->level[cell] == 1) return true;
+  if (present_closed_door(e, cell)) return true;
+  const int A = e.S->A;
+  bool b = e.lane < A && e.agpos()[e.lane] == cell && e.S->s.agent_blocking[e.lane];
+  return ballot(b) != 0;
+}
+// number of colliders in the global list at cell (walls, closed doors, agents)
+__device__ int colliders_at(const Env& e, int cell) {
+  int n = (e.S->level[cell] == 1) + (present_closed_door(e, cell) ? 1 : 0);
+  return n + popc(agents_at(e, cell));
+}
+// number of entities in the global list at cell (Door.tick, doors/entitites.py:109)
+__device__ int global_count(const Env& e, int cell) {
+  const int lane = e.lane;
+  int n = (e.S->level[cell] == 1);
+  int d = door_idx(e, cell);
+  if (d >= 0 && (e.door()[d] & DW_PRESENT)) n++;
+  n += popc(agents_at(e, cell));
+  n += popc(grp_at(e.items(), e.H(H_N_ITEMS), cell, EW_PRESENT, lane));
+  n += popc(grp_at(e.pods(), e.H(H_N_PODS), cell, EW_PRESENT, lane));
+  n += popc(grp_at(e.drops(), e.H(H_N_DROPS), cell, EW_PRESENT, lane));
+  n += popc(grp_at(e.dests(), e.H(H_N_DESTS), cell, EW_PRESENT, lane));
+  n += popc(grp_at(e.dirtpos(), e.H(H_N_DIRT), cell, EW_PRESENT, lane));
+  return n;
+}
+
+// ------------------------------------------------------------------------------------------------
+// spawn-position queries (global_entities.py:77-121)
+// ------------------------------------------------------------------------------------------------
+// a cell in the global list with no collider and no blocker (free_positions_generator)
+__device__ __forceinline__ bool lane_cell_free(const Env& e, int cell) {
+  if (present_closed_door(e, cell)) return false;
+  const int A = e.S->A;
+  for (int b = 0; b < A; b++)
+    if (e.agpos()[b] == cell) return false;
+  return true;
+}
+// a cell whose global list is empty (empty_positions)
+__device__ __forceinline__ bool lane_cell_empty(const Env& e, int cell) {
+  int d = door_idx(e, cell);
+  if (d >= 0 && (e.door()[d] & DW_PRESENT)) return false;
+  const int A = e.S->A;
+  for (int b = 0; b < A; b++)
+    if (e.agpos()[b] == cell) return false;
+  int n;
+  n = e.H(H_N_ITEMS);
+  for (int i = 0; i < n; i++) { int w = e.items()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
+  n = e.H(H_N_PODS);
+  for (int i = 0; i < n; i++) { int w = e.pods()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
+  n = e.H(H_N_DROPS);
+  for (int i = 0; i < n; i++) { int w = e.drops()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
+  n = e.H(H_N_DESTS);
+  for (int i = 0; i < n; i++) { int w = e.dests()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
+  n = e.H(H_N_DIRT);
+  for (int i = 0; i < n; i++) { int w = e.dirtpos()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
+  return true;
+}
+// first n free cells of a fresh floor shuffle -> out[0..k) (LDS scratch), returns k
+__device__ int free_positions(const Env& e, int n, int* out) {
+  floor_shuffle(e);
+  const uint16_t* perm = e.perm();
+  const int nf = e.S->nf;
+  int k = 0;
+  for (int b = 0; b < nf && k < n; b += MFG_WAVE) {
+    int i = b + e.lane;
+    int cell = i < nf ? (int)perm[i] : -1;
+    bool f = i < nf && lane_cell_free(e, cell);
+    u64 m = ballot(f);
+    int rank = k + popc(m & lt_mask());
+    if (f && rank < n) out[rank] = cell;
+    k += popc(m);
+  }
+  wave_sync();
+  return k < n ? k : n;
+}
+__device__ int spawn_positions(const Env& e, int n, int ignore_blocking, int* out) {
+  if (ignore_blocking) {  // floorlist[:n] (collection.py:368-369)
+    floor_shuffle(e);
+    int k = n < e.S->nf ? n : e.S->nf;
+    for (int i = e.lane; i < k; i += MFG_WAVE) out[i] = e.perm()[i];
+    wave_sync();
+    return k;
+  }
+  return free_positions(e, n, out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// spawning (collection.py:102-151 and the group overrides)
+// ------------------------------------------------------------------------------------------------
+// append one int-id entity to a group table; it enters the global pos_dict only if no entity with an
+// equal identifier is already there (Objects.notify_add_entity, objects.py:203-214)
+__device__ void spawn_into(const Env& e, int* tbl, int hn, int base, int cell) {
+  int n = e.H(hn);
+  int slot;
+  int id = base + n;
+  bool present = find_present_id(e, cell, id, &slot) == K_NONE;
+  if (e.lane == 0) tbl[n] = cell | EW_ALIVE | (present ? EW_PRESENT : 0);
+  e.setH(hn, n + 1);
+  wave_sync();
+}
+
+__device__ double dirt_global_amount(const Env& e) {  // clean_up/groups.py:27-32: left-to-right sum
+  double s = 0.0;
+  const int n = e.H(H_N_DIRT);
+  for (int i = 0; i < n; i++) s += e.dirtamt()[i];
+  return s;
+}
+
+#define DIRTPILE_MAX_LOCAL 5.0  /* DirtPile(max_local_amount=5): the collection value is never forwarded (Q20) */
+
+// DirtPiles.trigger_spawn (clean_up/groups.py:70-95); returns spawn_counter, *valid = result validity
+__device__ int dirt_trigger_spawn(const Env& e, int q, double amount, int* valid, int* scratch) {
+  const mfg_spec& s = e.S->s;
+  double u = pcg_uniform(e, -s.dirt_n_var, s.dirt_n_var);
+  int n_new = (int)fabs((double)q + u);
+  pay_debt(e);
+  int npos = free_positions(e, n_new, scratch);
+  // amounts: drawn for range(q) before any placement (numpy PCG64)
+  const int qa = q < MFG_WAVE ? q : MFG_WAVE;
+  double my_amt = amount;
+  for (int i = 0; i < qa; i++) {
+    double a = amount != 0.0 ? amount : s.dirt_initial_amount + pcg_uniform(e, -s.dirt_amount_var, s.dirt_amount_var);
+    if (e.lane == i) my_amt = a;
+  }
+  int n = npos < qa ? npos : qa;
+  int counter = 0;
+  for (int i = 0; i < n; i++) {
+    const int cell = scratch[i];
+    const double a = __shfl(my_amt, i);
+    if (dirt_global_amount(e) > s.dirt_max_global) { *valid = 0; return counter; }
+    const int nd = e.H(H_N_DIRT);
+    u64 m = grp_at(e.dirtpos(), nd, cell, EW_ALIVE, e.lane);
+    if (m) {
+      const int k = ffs64(m);
+      double nv = e.dirtamt()[k] + a;
+      wave_sync();
+      if (e.lane == 0) e.dirtamt()[k] = nv < DIRTPILE_MAX_LOCAL ? nv : DIRTPILE_MAX_LOCAL;
+      wave_sync();
+    } else {
+      if (nd >= MFG_DIRT_MAX) { e.setH(H_OVERFLOW, 1); *valid = 0; return counter; }
+      int id = e.H(H_CNT_DIRT);
+      int slot;
+      bool present = find_present_id(e, cell, id, &slot) == K_NONE;
+      if (e.lane == 0) {
+        e.dirtpos()[nd] = cell | EW_ALIVE | (present ? EW_PRESENT : 0);
+        e.dirtid()[nd] = id;
+        e.dirtamt()[nd] = a;
+      }
+      e.setH(H_CNT_DIRT, id + 1);
+      e.setH(H_N_DIRT, nd + 1);
+      wave_sync();
+      counter++;
+    }
+  }
+  *valid = 1;
+  return counter;
+}
+
+// remove dirt slot k keeping collection order (Collection.__delitem__)
+__device__ void dirt_delete(const Env& e, int k) {
+  const int nd = e.H(H_N_DIRT);
+  const int cell = EW_POS(e.dirtpos()[k]);
+  const int id = e.dirtid()[k];
+  global_remove_id(e, cell, id);
+  int p = 0, i = 0;
+  double a = 0.0;
+  if (e.lane < nd && e.lane != k) { p = e.dirtpos()[e.lane]; i = e.dirtid()[e.lane]; a = e.dirtamt()[e.lane]; }
+  wave_sync();
+  if (e.lane < nd && e.lane != k) {
+    int dst = e.lane > k ? e.lane - 1 : e.lane;
+    e.dirtpos()[dst] = p; e.dirtid()[dst] = i; e.dirtamt()[dst] = a;
+  }
+  e.setH(H_N_DIRT, nd - 1);
+  wave_sync();
+}
+
+// ------------------------------------------------------------------------------------------------
+// step bookkeeping: rewards are accumulated per agent in the reference's result order
+// ------------------------------------------------------------------------------------------------
+struct StepOut {
+  double my_rew;      // lane a: agent a's reward sum so far
+  double g_rew;       // uniform: 'global' reward sum
+  int my_act_ev;      // lane a: act event bits
+  int my_watch_ev;    // lane a: watch event bits
+  uint64_t door_coll;
+  int respawn_items_value, dirt_spawn_value, dirt_spawn_valid, door_autoclose, done_mask, dest_pack, crashed;
+  int done;
+};
+
+__device__ __forceinline__ void add_agent_reward(const Env& e, StepOut& o, int a, double r) {
+  if (e.lane == a) o.my_rew += r;
+}
+
+__device__ const mfg_action& action_of(const Env& e, int a, int slot) { return e.S->s.actions[a][slot]; }
+
+__device__ __forceinline__ void set_agent_pos(const Env& e, int a, int cell) {
+  wave_sync();
+  if (e.lane == 0) {
+    e.agpos()[a] = cell;
+    int c = e.hdr()[H_ARRIVAL];
+    e.agarr()[a] = c;
+    e.hdr()[H_ARRIVAL] = c + 1;
+  }
+  wave_sync();
+}
+
+// ------------------------------------------------------------------------------------------------
+// actions (environment/actions.py, modules/*/actions.py)
+// ------------------------------------------------------------------------------------------------
+__device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
+  const MfgDevSpec* S = e.S;
+  const mfg_action& ac = action_of(e, a, slot);
+  const int op = ac.op;
+  const int pos = uni(e.agpos()[a]);
+  const int W = S->s.W;
+  const int x = pos / W, y = pos % W;
+  int valid = 0, coll = 0, aux = 0;
+  if (op == MFG_ACT_NOOP) {
+    valid = 1;
+  } else if (op == MFG_ACT_MOVE) {  // actions.py:77-100, states.py:240-270, entity.py:175-199
+    static const int DX[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
+    static const int DY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+    const int nx = x + DX[ac.arg], ny = y + DY[ac.arg];
+    const int t = nx * W + ny;  // levels are wall-bounded: a move never leaves the grid
+    const bool blocked = blocked_at(e, t);
+    int debt = 0;
+    if (!blocked) debt++;  // check_pos_validity -> `pos in floorlist` shuffles (Q3)
+    const bool not_blocked = !blocked && S->level[t] != 1;
+    bool blocking_others = false;
+    if (S->s.agent_blocking[a]) blocking_others = colliders_at(e, t) > 0 || blocked;  // is_occupied
+    const bool v = pos != t && not_blocked && !blocking_others;
+    if (v) {
+      debt++;  // Entity.move re-checks validity (second shuffle)
+      set_agent_pos(e, a, t);
+      valid = 1;
+      coll = colliders_at(e, t) > 1;
+    } else {
+      valid = 0;
+      coll = 1;
+    }
+    e.setH(H_DEBT, e.H(H_DEBT) + debt);
+    wave_sync();
+  } else if (op == MFG_ACT_DOORUSE) {  // doors/actions.py:18-34; global_entities.py:13-38
+    static const int MX[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
+    static const int MY[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
+    u64 toggle = 0;
+    for (int k = 0; k < 9; k++) {
+      const int px = x + MX[k], py = y + MY[k];
+      if (px < 0 || py < 0 || px >= S->s.H || py >= W) continue;
+      const int c = px * W + py;
+      if (S->level[c] == 1) continue;
+      const int d = door_idx(e, c);
+      if (d >= 0 && (e.door()[d] & DW_PRESENT)) toggle |= 1ull << d;
+    }
+    if (toggle) {
+      valid = 1;
+      wave_sync();
+      if (e.lane < S->nd && ((toggle >> e.lane) & 1)) {
+        int w = e.door()[e.lane];
+        if (w & DW_OPEN) w &= ~DW_OPEN;
+        else w = (w & DW_PRESENT) | DW_OPEN | ((S->s.door_auto_close & 0xFF) << 8);
+        e.door()[e.lane] = w;
+      }
+      wave_sync();
+    }
+  } else if (op == MFG_ACT_ITEM) {  // items/actions.py:41-63
+    if (grp_at(e.drops(), e.H(H_N_DROPS), pos, EW_ALIVE, e.lane)) {
+      valid = 0;  // inventories are always empty (pickup bug, Q8)
+      aux = 1;
+    } else {
+      u64 m = grp_at(e.items(), e.H(H_N_ITEMS), pos, EW_ALIVE, e.lane);
+      if (m) {
+        const int k = ffs64(m);
+        global_remove_id(e, pos, e.H(H_ITEM_BASE) + k);
+        if (e.lane == 0) e.items()[k] = (e.items()[k] & ~0xFFFF) | EW_NOPOS;
+        wave_sync();
+        valid = 1;
+      }
+    }
+  } else if (op == MFG_ACT_CHARGE) {  // batteries/actions.py:20-31, entitites.py:98-111
+    if (grp_at(e.pods(), e.H(H_N_PODS), pos, EW_ALIVE, e.lane)) {
+      const double ch = e.bat()[a];
+      if (ch >= 1.0) valid = 0;
+      else if (popc(agents_at(e, pos)) > 1) valid = 0;
+      else {
+        const double nv = S->s.pod_charge_rate + ch;
+        wave_sync();
+        if (e.lane == 0) e.bat()[a] = nv > 1.0 ? 1.0 : nv;
+        wave_sync();
+        valid = 1;
+      }
+    }
+  } else if (op == MFG_ACT_CLEAN) {  // clean_up/actions.py:19-36
+    u64 m = grp_at(e.dirtpos(), e.H(H_N_DIRT), pos, EW_PRESENT, e.lane);
+    if (m) {
+      const int k = ffs64(m);
+      const double na = e.dirtamt()[k] - S->s.dirt_clean_amount;
+      if (na <= 0) {
+        dirt_delete(e, k);
+      } else {
+        wave_sync();
+        if (e.lane == 0) e.dirtamt()[k] = na < DIRTPILE_MAX_LOCAL ? na : DIRTPILE_MAX_LOCAL;
+        wave_sync();
+      }
+      valid = 1;
+    }
+  } else if (op == MFG_ACT_DEST) {  // destinations/actions.py:17-24
+    if (grp_at(e.dests(), e.H(H_N_DESTS), pos, EW_ALIVE, e.lane)) {
+      o.crashed = 1;  // AttributeError upstream (Q17)
+      return;
+    }
+    valid = 0;
+  }
+  const double rw = aux ? (valid ? ac.aux0 : ac.aux1) : (valid ? ac.valid_reward : ac.fail_reward);
+  add_agent_reward(e, o, a, rw);
+  if (e.lane == a) o.my_act_ev = 0x80 | (valid ? 1 : 0) | (coll ? 2 : 0) | (aux ? 4 : 0);
+}
+
+// ------------------------------------------------------------------------------------------------
+// rules (environment/rules.py, modules/*/rules.py); hook order states.py:170-226
+// ------------------------------------------------------------------------------------------------
+__device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
+  const MfgDevSpec* S = e.S;
+  const mfg_rule& ru = S->s.rules[ri];
+  const int op = ru.op;
+  if (op == MFG_RULE_DOOR_AUTOCLOSE) {  // doors/rules.py:20-28, doors/entitites.py:107-122
+    if (S->nd > 0) {
+      const int nd = S->nd;
+      int cnt = 0;
+      for (int d = 0; d < nd; d++) {  // global_count uses ballots: evaluate per door uniformly
+        int c = global_count(e, S->door_cells[d]);
+        if (e.lane == d) cnt = c;
+      }
+      wave_sync();
+      if (e.lane < nd) {
+        int w = e.door()[e.lane];
+        if (cnt <= 2) {
+          const int ttc = DW_TTC(w);
+          if ((w & DW_OPEN) && ttc) w = (w & ~0xFF00) | ((ttc - 1) << 8);
+          else if ((w & DW_OPEN) && !ttc) w &= ~DW_OPEN;
+        } else {
+          w = (w & ~0xFF00) | ((S->s.door_auto_close & 0xFF) << 8);
+        }
+        e.door()[e.lane] = w;
+      }
+      wave_sync();
+      o.door_autoclose = 1;
+    }
+  } else if (op == MFG_RULE_RESPAWN_ITEMS) {  // items/rules.py:28-33
+    int c = uni(e.rctr()[ri]);
+    if (!c) {
+      if (S->s.items_quantity - e.H(H_N_ITEMS) > 0) o.crashed = 1;  // Item(pos, n, freq) TypeError upstream
+    } else {
+      wave_sync();
+      if (e.lane == 0) e.rctr()[ri] = c - 1 > 0 ? c - 1 : 0;
+      wave_sync();
+    }
+  } else if (op == MFG_RULE_BATTERY_DECHARGE || op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:50-64
+    if (e.lane < S->A) {
+      double b = e.bat()[e.lane];
+      if (b != 0.0) {
+        double nv = ru.f[0] + b;
+        e.bat()[e.lane] = nv > 0.0 ? nv : 0.0;
+      }
+    }
+    wave_sync();
+  } else if (op == MFG_RULE_RESPAWN_DIRT) {  // clean_up/rules.py:49-59
+    int c = uni(e.rctr()[ri]);
+    if (c < 0) {
+    } else if (!c) {
+      int valid;
+      int v = dirt_trigger_spawn(e, ru.i[1], ru.f[0], &valid, scratch);
+      o.dirt_spawn_value = v;
+      o.dirt_spawn_valid = valid;
+      wave_sync();
+      if (e.lane == 0) e.rctr()[ri] = ru.i[0];
+      wave_sync();
+    } else {
+      wave_sync();
+      if (e.lane == 0) e.rctr()[ri] = c - 1;
+      wave_sync();
+    }
+  } else if (op == MFG_RULE_DEST_REACH || op == MFG_RULE_DONE_DEST) {  // destinations/rules.py:34-54
+    const int n = e.H(H_N_DESTS);
+    for (int i = 0; i < n; i++) {
+      const int w = uni(e.dests()[i]);
+      if (w & EW_REACHED) continue;
+      const int cell = EW_POS(w);
+      const u64 am = agents_at(e, cell);
+      if (!am) continue;
+      // the Agents-group cell list is in arrival order; the loop variable ends on the last arrival
+      int arr = e.lane < S->A && ((am >> e.lane) & 1) ? e.agarr()[e.lane] : -1;
+      int best = arr;
+      for (int o2 = 32; o2 > 0; o2 >>= 1) best = max(best, __shfl_xor(best, o2));
+      const u64 lm = ballot(arr == best && arr >= 0);
+      const int last = ffs64(lm);
+      wave_sync();
+      if (e.lane == 0) e.dests()[i] = w | EW_REACHED;
+      wave_sync();
+      add_agent_reward(e, o, last, ru.f[0]);
+      for (int k = 0; k < 4; k++)
+        if (((o.dest_pack >> (8 * k)) & 0xFF) == 0) { o.dest_pack |= (last + 1) << (8 * k); break; }
+    }
+  }
+}
+
+__device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
+  const MfgDevSpec* S = e.S;
+  const mfg_rule& ru = S->s.rules[ri];
+  const int op = ru.op;
+  if (op == MFG_RULE_RESPAWN_ITEMS) {  // items/rules.py:35-43
+    int c = uni(e.rctr()[ri]);
+    if (!c) {
+      if (S->s.items_quantity - e.H(H_N_ITEMS) > 0) { o.crashed = 1; return; }
+      o.respawn_items_value = S->s.items_quantity;
+    } else {
+      wave_sync();
+      if (e.lane == 0) e.rctr()[ri] = c - 1 > 0 ? c - 1 : 0;
+      wave_sync();
+    }
+  } else if (op == MFG_RULE_WATCH_COLLISIONS) {  // rules.py:276-307
+    // cells with >= 2 colliders: agent cells (agents, closed doors); every collider there gets one result
+    const int A = S->A;
+    bool hit = false;
+    for (int a = 0; a < A; a++) {
+      const int cell = uni(e.agpos()[a]);
+      const int n = colliders_at(e, cell);
+      if (n >= 2) {
+        hit = true;
+        if (e.lane == a) {
+          if (!(o.my_watch_ev & 1)) o.my_rew += ru.f[0];
+          o.my_watch_ev |= 1;
+        }
+        const int d = door_idx(e, cell);
+        if (d >= 0 && present_closed_door(e, cell)) o.door_coll |= 1ull << d;
+      }
+    }
+    if (ru.i[0] && hit) o.done_mask |= (int)(1u << 31);  // curr_done -> on_check_done
+  } else if (op == MFG_RULE_BATTERY_DECHARGE || op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:66-87
+    if (e.lane < S->A) {
+      const bool dis = e.bat()[e.lane] == 0.0;
+      int par = e.agpar()[e.lane];
+      if (dis) {
+        o.my_rew += ru.f[1];
+        o.my_watch_ev |= 2;
+        if (ru.i[0]) par |= 1 << ri;
+      }
+      if (par && !dis) par &= ~(1 << ri);
+      e.agpar()[e.lane] = par;
+    }
+    wave_sync();
+  }
+}
+
+__device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
+  const MfgDevSpec* S = e.S;
+  const mfg_rule& ru = S->s.rules[ri];
+  const int op = ru.op;
+  if (op == MFG_RULE_DONE_MAXSTEPS) {
+    if (ru.i[0] <= e.H(H_STEP)) { o.done = 1; o.done_mask |= 1 << ri; }
+  } else if (op == MFG_RULE_WATCH_COLLISIONS) {
+    if (ru.i[0] && (o.done_mask & (int)(1u << 31))) { o.done = 1; o.g_rew += ru.f[1]; }
+  } else if (op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:122-128
+    const bool dz = e.lane < S->A && e.bat()[e.lane] == 0.0;
+    const u64 m = ballot(dz);
+    const bool any = m != 0;
+    const bool all = popc(m) == S->A;
+    if (ru.i[1] && (any || all)) { o.done = 1; o.done_mask |= 1 << ri; o.g_rew += ru.f[2]; }
+  } else if (op == MFG_RULE_DONE_DIRT) {  // clean_up/rules.py:22-25
+    if (e.H(H_N_DIRT) == 0 && e.H(H_STEP)) { o.done = 1; o.done_mask |= 1 << ri; o.g_rew += ru.f[0]; }
+  } else if (op == MFG_RULE_DONE_DEST) {  // destinations/rules.py:73-92
+    const int n = e.H(H_N_DESTS);
+    const bool rr = e.lane < n && (e.dests()[e.lane < n ? e.lane : 0] & EW_REACHED);
+    const u64 m = ballot(rr);
+    const bool any = m != 0, all = popc(m) == n;
+    const int cond = ru.i[0];
+    if ((cond == MFG_DEST_ANY && any) || (cond != MFG_DEST_ANY && all)) {
+      o.done = 1; o.done_mask |= 1 << ri; o.g_rew += ru.f[1];
+    } else if (cond == MFG_DEST_SIMULTANEOUS) {
+      wave_sync();
+      if (e.lane < n) e.dests()[e.lane] &= ~EW_REACHED;
+      wave_sync();
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// reset (factory.py:134-148; global_entities.py:196-203; rules.py:182-199; SpawnEntity rules)
+// ------------------------------------------------------------------------------------------------
+__device__ void env_reset(const Env& e, int* scratch) {
+  const MfgDevSpec* S = e.S;
+  const int A = S->A;
+  pay_debt(e);
+  // OBSBuilder keeps the episode-1 agent / battery objects for its ray origins and bound layers
+  if (e.H(H_OBS_INIT) && !e.H(H_FROZEN)) {
+    if (e.lane < A) {
+      e.forg()[e.lane] = e.agpos()[e.lane];
+      e.fgp()[e.lane] = e.agpos()[e.lane];
+      e.fbat()[e.lane] = e.bat()[e.lane];
+    }
+    e.setH(H_FROZEN, 1);
+  }
+  e.setH(H_STEP, 0);
+  e.setH(H_CRASHED, 0);
+  e.setH(H_N_ITEMS, 0); e.setH(H_N_PODS, 0); e.setH(H_N_DROPS, 0); e.setH(H_N_DIRT, 0); e.setH(H_N_DESTS, 0);
+  if (e.lane < S->nd) e.door()[e.lane] = DW_PRESENT | ((S->s.door_auto_close & 0xFF) << 8);  // closed
+  if (e.lane < A) { e.agpos()[e.lane] = -1; e.agpar()[e.lane] = 0; }
+  wave_sync();
+  // SpawnAgents: per agent empty_positions (floor shuffle + filter + shuffle of the list) then pop()
+  for (int a = 0; a < A; a++) {
+    floor_shuffle(e);
+    const uint16_t* perm = e.perm();
+    const int nf = S->nf;
+    int m = 0;
+    for (int b = 0; b < nf; b += MFG_WAVE) {
+      const int i = b + e.lane;
+      const bool em = i < nf && lane_cell_empty(e, perm[i < nf ? i : 0]);
+      m += popc(ballot(em));
+    }
+    const int j = mt_randbelow_seq(e, m - 1, m - 1, nullptr);  // first Fisher-Yates step picks the last slot
+    if (m - 2 >= 1) mt_randbelow_seq(e, m - 2, 1, nullptr);     // remaining draws of shuffle(empty_positions)
+    int k = 0, cell = -1;
+    for (int b = 0; b < nf && cell < 0; b += MFG_WAVE) {
+      const int i = b + e.lane;
+      const bool em = i < nf && lane_cell_empty(e, perm[i < nf ? i : 0]);
+      const u64 mm = ballot(em);
+      const int rank = k + popc(mm & lt_mask());
+      const u64 hitm = ballot(em && rank == j);
+      if (hitm) cell = rl(i < nf ? (int)perm[i] : 0, ffs64(hitm));
+      k += popc(mm);
+    }
+    wave_sync();
+    if (e.lane == 0) { e.agpos()[a] = cell; e.agarr()[a] = a; }
+    e.setH(H_CNT_AGENT, e.H(H_CNT_AGENT) + 1);
+    wave_sync();
+  }
+  e.setH(H_ARRIVAL, A);
+  // rules' on_reset in order (states.py:45-50)
+  for (int r = 0; r < S->s.n_rules; r++) {
+    const mfg_rule& ru = S->s.rules[r];
+    const int op = ru.op;
+    if (op == MFG_RULE_SPAWN_BATTERIES) {
+      e.setH(H_BAT_BASE, e.H(H_CNT_BATTERY));
+      e.setH(H_CNT_BATTERY, e.H(H_CNT_BATTERY) + A);
+      if (e.lane < A) e.bat()[e.lane] = S->s.battery_initial;
+      wave_sync();
+    } else if (op == MFG_RULE_SPAWN_PODS || op == MFG_RULE_SPAWN_DROPOFFS || op == MFG_RULE_SPAWN_ITEMS ||
+               op == MFG_RULE_SPAWN_DESTS) {
+      int hn, hb, hc;
+      int* tbl;
+      int q = ru.i[0];
+      if (op == MFG_RULE_SPAWN_PODS) { hn = H_N_PODS; hb = H_POD_BASE; hc = H_CNT_POD; tbl = e.pods(); }
+      else if (op == MFG_RULE_SPAWN_DROPOFFS) { hn = H_N_DROPS; hb = H_DROP_BASE; hc = H_CNT_DROP; tbl = e.drops(); }
+      else if (op == MFG_RULE_SPAWN_DESTS) { hn = H_N_DESTS; hb = H_DEST_BASE; hc = H_CNT_DEST; tbl = e.dests(); }
+      else { hn = H_N_ITEMS; hb = H_ITEM_BASE; hc = H_CNT_ITEM; tbl = e.items(); q -= e.H(H_N_ITEMS); }
+      if (q > 0) {
+        const int n = spawn_positions(e, q, ru.i[1], scratch);
+        const int base = e.H(hc);
+        e.setH(hb, base);
+        for (int i = 0; i < n; i++) spawn_into(e, tbl, hn, base, scratch[i]);
+        e.setH(hc, base + n);
+        wave_sync();
+      }
+    } else if (op == MFG_RULE_SPAWN_DIRT) {
+      int v;
+      dirt_trigger_spawn(e, S->s.dirt_quantity, 0.0, &v, scratch);
+    } else if (op == MFG_RULE_SPAWN_GLOBALPOS) {
+      e.setH(H_CNT_GP, e.H(H_CNT_GP) + A);
+    } else if (op == MFG_RULE_SPAWN_MACHINES || op == MFG_RULE_SPAWN_MAINTAINERS) {
+      e.setH(H_CRASHED, 1);  // not compiled into specs (spec.py rejects), defensive
+    }
+    wave_sync();
+  }
+  e.setH(H_EPISODE, e.H(H_EPISODE) + 1);
+  wave_sync();
+}
+
+// ------------------------------------------------------------------------------------------------
+// observation (observation_builder.py:138-235, ray_caster.py:66-104)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
+  const MfgDevSpec* S = e.S;
+  if (x < 0 || y < 0 || x >= S->s.H || y >= S->s.W) return false;
+  const int c = x * S->s.W + y;
+  if (S->level[c] == 1) return true;
+  return present_closed_door(e, c);
+}
+
+template <int MAXPTS>
+struct RayVis {
+  int cell[MAXPTS];  // visible cells of this lane's ray (-1 if none/not visible)
+};
+
+// rank of the first visit of `cell` (ray index * 32 + point index), or a large value if not visible
+template <int MAXPTS>
+__device__ int first_visit(const RayVis<MAXPTS>& rv, int cell) {
+  int k = -1;
+#pragma unroll
+  for (int p = 0; p < MAXPTS; p++)
+    if (k < 0 && rv.cell[p] == cell) k = p;
+  const u64 m = ballot(k >= 0);
+  if (!m) return 1 << 30;
+  const int L = ffs64(m);
+  return L * 32 + rl(k, L);
+}
+
+template <int MAXPTS, typename OT>
+__device__ void build_obs(const Env& e, OT* out_env) {
+  const MfgDevSpec* S = e.S;
+  const int A = S->A, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
+  const int lane = e.lane;
+  const bool frozen = e.H(H_FROZEN) != 0;
+  for (int a = 0; a < A; a++) {
+    const int apos = uni(e.agpos()[a]);
+    const int ax = apos / W, ay = apos % W;
+    const int org = frozen ? uni(e.forg()[a]) : apos;
+    const int ox = org / W, oy = org % W;
+    // ---- ray walk: lane = ray ----
+    RayVis<MAXPTS> rv;
+    u64 wmask = 0;
+    {
+      const bool has = lane < S->nrays;
+      const int len = has ? S->ray_len[lane] : 0;
+      const int8_t* pts = S->ray_pts + (size_t)(has ? lane : 0) * MAXPTS * 2;
+      bool alive = has;
+      int rx = ox, ry = oy;
+#pragma unroll
+      for (int p = 0; p < MAXPTS; p++) {
+        rv.cell[p] = -1;
+        if (alive && p < len) {
+          const int x = ox + pts[2 * p], y = oy + pts[2 * p + 1];
+          const int cx = x - rx, cy = y - ry;
+          const bool hits = light_block(e, x, y);
+          const bool diag = (cx != 0 && cy != 0) ? (light_block(e, x, y - cy) && light_block(e, x - cx, y)) : false;
+          if (!diag && x >= 0 && y >= 0 && x < S->s.H && y < W) {
+            rv.cell[p] = x * W + y;
+            const int px = x - ax + r, py = y - ay + r;
+            if (px >= 0 && py >= 0 && px < d && py < d) wmask |= 1ull << (px * d + py);
+          }
+          if (hits || diag) alive = false;
+          rx = x;
+          ry = y;
+        }
+      }
+    }
+    const u64 vis = wave_or64(wmask);
+    // ---- identifier-collision dedupe (set(visible_entities), Q14): the later first-visit loses ----
+    // candidates: int-id entities within reach of the origin whose identifier is shared with another
+    // class (walls 0..nw-1 and doors 0..nd-1 are static; dynamic groups carry their base ids).
+    u64 sup_items = 0, sup_pods = 0, sup_drops = 0, sup_dests = 0, sup_dirt = 0, sup_doors = 0;
+    int sup_walls[8];
+    int n_sup_walls = 0;
+    {
+      const int reach = d;  // rays walk radius d = 2r+1 (Q13)
+      auto near = [&](int cell) {
+        const int x = cell / W, y = cell % W;
+        return abs(x - ox) <= reach && abs(y - oy) <= reach;
+      };
+      // (class, slot, id, cell) of present int-id entities; walls/doors handled via id ranges
+      const int nw = S->nw, ndr = S->nd;
+      const int groups = 5;
+      for (int g = 0; g < groups; g++) {
+        const int* tbl = g == 0 ? e.items() : g == 1 ? e.pods() : g == 2 ? e.drops() : g == 3 ? e.dests() : e.dirtpos();
+        const int n = e.H(g == 0 ? H_N_ITEMS : g == 1 ? H_N_PODS : g == 2 ? H_N_DROPS : g == 3 ? H_N_DESTS : H_N_DIRT);
+        const int base = g == 0 ? e.H(H_ITEM_BASE) : g == 1 ? e.H(H_POD_BASE) : g == 2 ? e.H(H_DROP_BASE)
+                       : g == 3 ? e.H(H_DEST_BASE) : 0;
+        for (int i = 0; i < n; i++) {
+          const int w = uni(tbl[i]);
+          if (!(w & EW_PRESENT)) continue;
+          const int cell = EW_POS(w);
+          if (!near(cell)) continue;
+          const int id = g == 4 ? uni(e.dirtid()[i]) : base + i;
+          const int rE = first_visit<MAXPTS>(rv, cell);
+          if (rE >= (1 << 30)) continue;
+          // partners: wall, door, and entities of later groups with the same id
+          bool lose = false;
+          if (id < nw) {
+            const int wc = S->wall_cells[id];
+            if (near(wc)) {
+              const int rW = first_visit<MAXPTS>(rv, wc);
+              if (rW < rE) lose = true;
+              else if (rW < (1 << 30) && n_sup_walls < 8) sup_walls[n_sup_walls++] = wc;
+            }
+          }
+          if (id < ndr && (e.door()[id] & DW_PRESENT)) {
+            const int dc = S->door_cells[id];
+            if (near(dc)) {
+              const int rD = first_visit<MAXPTS>(rv, dc);
+              if (rD < rE) lose = true;
+              else if (rD < (1 << 30)) sup_doors |= 1ull << id;
+            }
+          }
+          for (int g2 = g + 1; g2 < groups; g2++) {
+            const int* t2 = g2 == 1 ? e.pods() : g2 == 2 ? e.drops() : g2 == 3 ? e.dests() : e.dirtpos();
+            const int n2 = e.H(g2 == 1 ? H_N_PODS : g2 == 2 ? H_N_DROPS : g2 == 3 ? H_N_DESTS : H_N_DIRT);
+            const int b2 = g2 == 1 ? e.H(H_POD_BASE) : g2 == 2 ? e.H(H_DROP_BASE) : g2 == 3 ? e.H(H_DEST_BASE) : 0;
+            for (int j = 0; j < n2; j++) {
+              const int w2 = uni(t2[j]);
+              if (!(w2 & EW_PRESENT)) continue;
+              const int id2 = g2 == 4 ? uni(e.dirtid()[j]) : b2 + j;
+              if (id2 != id) continue;
+              const int c2 = EW_POS(w2);
+              if (!near(c2)) continue;
+              const int r2 = first_visit<MAXPTS>(rv, c2);
+              if (r2 >= (1 << 30)) continue;
+              u64 bit = 1ull << j;
+              if (r2 < rE) lose = true;
+              else if (g2 == 1) sup_pods |= bit;
+              else if (g2 == 2) sup_drops |= bit;
+              else if (g2 == 3) sup_dests |= bit;
+              else sup_dirt |= bit;
+            }
+          }
+          if (lose) {
+            const u64 bit = 1ull << i;
+            if (g == 0) sup_items |= bit;
+            else if (g == 1) sup_pods |= bit;
+            else if (g == 2) sup_drops |= bit;
+            else if (g == 3) sup_dests |= bit;
+            else sup_dirt |= bit;
+          }
+        }
+      }
+      // static Wall[k] / Door[k] pairs
+      const int kmax = nw < ndr ? nw : ndr;
+      for (int k = 0; k < kmax; k++) {
+        if (!(e.door()[k] & DW_PRESENT)) continue;
+        const int wc = S->wall_cells[k], dc = S->door_cells[k];
+        if (!near(wc) || !near(dc)) continue;
+        const int rW = first_visit<MAXPTS>(rv, wc), rD = first_visit<MAXPTS>(rv, dc);
+        if (rW >= (1 << 30) || rD >= (1 << 30)) continue;
+        if (rW < rD) sup_doors |= 1ull << k;
+        else if (n_sup_walls < 8) sup_walls[n_sup_walls++] = wc;
+      }
+    }
+    // ---- placement: lane = window cell ----
+    {
+      const bool inwin = lane < dd;
+      const int px = lane / d, py = lane % d;
+      const int x = ax - r + px, y = ay - r + py;
+      const bool ing = inwin && x >= 0 && y >= 0 && x < S->s.H && y < W;
+      const int cell = ing ? x * W + y : -1;
+      const bool v = inwin && ((vis >> lane) & 1) && ing;
+      // per-tag values at this cell
+      double t_wall = 0, t_door = 0, t_item = 0, t_pod = 0, t_drop = 0, t_dirt = 0, t_dest = 0;
+      u64 amask = 0;
+      if (v) {
+        if (S->level[cell] == 1) {
+          bool s = false;
+          for (int q = 0; q < n_sup_walls; q++) s |= sup_walls[q] == cell;
+          if (!s) t_wall = 1.0;
+        }
+        const int dI = door_idx(e, cell);
+        if (dI >= 0) {
+          const int w = e.door()[dI];
+          if ((w & DW_PRESENT) && !((sup_doors >> dI) & 1)) t_door = (w & DW_OPEN) ? 0.4444 : 0.6666;
+        }
+        for (int b = 0; b < A; b++)
+          if (e.agpos()[b] == cell) amask |= 1ull << b;
+        int n = e.H(H_N_ITEMS);
+        for (int i = 0; i < n; i++) {
+          const int w = e.items()[i];
+          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_items >> i) & 1)) t_item += 1.0;
+        }
+        n = e.H(H_N_PODS);
+        for (int i = 0; i < n; i++) {
+          const int w = e.pods()[i];
+          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_pods >> i) & 1)) t_pod += 1.0;
+        }
+        n = e.H(H_N_DROPS);
+        for (int i = 0; i < n; i++) {
+          const int w = e.drops()[i];
+          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_drops >> i) & 1)) t_drop += 1.0;
+        }
+        n = e.H(H_N_DESTS);
+        for (int i = 0; i < n; i++) {
+          const int w = e.dests()[i];
+          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_dests >> i) & 1)) t_dest += (w & EW_REACHED) ? 0.0 : 1.0;
+        }
+        n = e.H(H_N_DIRT);
+        for (int i = 0; i < n; i++) {
+          const int w = e.dirtpos()[i];
+          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_dirt >> i) & 1)) t_dirt += e.dirtamt()[i];
+        }
+      }
+      auto tagv = [&](int tag) -> double {
+        switch (tag) {
+          case MFG_TAG_WALLS: return t_wall;
+          case MFG_TAG_DOORS: return t_door;
+          case MFG_TAG_ITEMS: return t_item;
+          case MFG_TAG_PODS: return t_pod;
+          case MFG_TAG_DROPOFFS: return t_drop;
+          case MFG_TAG_DIRT: return t_dirt;
+          case MFG_TAG_DESTS: return t_dest;
+          default:
+            if (tag >= MFG_TAG_AGENT0) return ((amask >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
+            return 0.0;
+        }
+      };
+      OT* out_a = out_env + (size_t)a * S->obs_agent_stride;
+      const int nl = S->s.n_layers[a];
+      for (int l = 0; l < nl; l++) {
+        const mfg_layer& ly = S->s.layers[a][l];
+        double val = 0.0;
+        if (ly.kind == MFG_LAYER_TAG) {
+          val = tagv(ly.tag);
+        } else if (ly.kind == MFG_LAYER_COMBINED) {
+          const int nc = S->s.combined_n[a];
+          for (int q = 0; q < nc; q++) val = q == 0 ? tagv(S->s.combined_tags[a][q]) : val + tagv(S->s.combined_tags[a][q]);
+        } else if (ly.kind == MFG_LAYER_BATTERY) {
+          if (lane == 0) val = frozen ? e.fbat()[a] : e.bat()[a];
+        } else if (ly.kind == MFG_LAYER_GLOBALPOS) {
+          const int gp = frozen ? e.fgp()[a] : apos;
+          if (lane == 0) val = (double)(gp / W) / (double)S->s.H;
+          if (lane == 1) val = (double)(gp % W) / (double)W;
+        }
+        if (inwin) out_a[(size_t)l * dd + lane] = (OT)val;
+      }
+      // padding layers (agents with fewer layers than lmax) stay untouched: zeroed once by the host
+    }
+  }
+  e.setH(H_OBS_INIT, 1);
+  wave_sync();
+}
+
+// ------------------------------------------------------------------------------------------------
+// one env-step (Factory.step, factory.py:189-220; Gamestate.tick, states.py:170-203)
+// ------------------------------------------------------------------------------------------------
+#define MFG_EV_MISC 10
+
+__device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
+  const MfgDevSpec* S = e.S;
+  const int A = S->A;
+  o.my_rew = 0.0; o.g_rew = 0.0; o.my_act_ev = 0; o.my_watch_ev = 0; o.door_coll = 0;
+  o.respawn_items_value = -1; o.dirt_spawn_value = -1; o.dirt_spawn_valid = 0; o.door_autoclose = 0;
+  o.done_mask = 0; o.dest_pack = 0; o.crashed = 0; o.done = 0;
+  e.setH(H_STEP, e.H(H_STEP) + 1);
+  e.setH(H_TOTAL_STEPS, e.H(H_TOTAL_STEPS) + 1);
+  wave_sync();
+  for (int a = 0; a < A && !o.crashed; a++) {
+    if (uni(e.agpar()[a])) continue;  // paralyzed agents skip their action
+    const int slot = rl(my_act, a);
+    do_action(e, o, a, slot);
+  }
+  const int nr = S->s.n_rules;
+  if (!o.crashed)
+    for (int r = 0; r < nr && !o.crashed; r++) rule_tick_step(e, o, r, scratch);
+  if (!o.crashed)
+    for (int r = 0; r < nr && !o.crashed; r++) rule_post_step(e, o, r);
+  if (!o.crashed)
+    for (int r = 0; r < nr; r++) rule_check_done(e, o, r);
+  pay_debt(e);  // eager replay of this step's membership-only shuffles
+  if (o.crashed || e.H(H_OVERFLOW)) {
+    o.crashed = 1;
+    o.done = 1;
+    e.setH(H_CRASHED, 1);
+  }
+  wave_sync();
+}
+
+__device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& o, size_t row, double* reward,
+                                                   uint8_t* done, uint8_t* ev_act, uint8_t* ev_watch,
+                                                   int32_t* ev_misc) {
+  const int A = e.S->A;
+  if (e.lane < A) {
+    if (reward) reward[row * A + e.lane] = o.my_rew + o.g_rew;
+    if (ev_act) ev_act[row * A + e.lane] = (uint8_t)o.my_act_ev;
+    if (ev_watch) ev_watch[row * A + e.lane] = (uint8_t)o.my_watch_ev;
+  }
+  if (e.lane == 0) {
+    if (done) done[row] = (uint8_t)o.done;
+    if (ev_misc) {
+      int32_t* m = ev_misc + row * MFG_EV_MISC;
+      m[0] = (int32_t)(uint32_t)o.door_coll;
+      m[1] = (int32_t)(uint32_t)(o.door_coll >> 32);
+      m[2] = o.respawn_items_value;
+      m[3] = o.dirt_spawn_value;
+      m[4] = o.dirt_spawn_valid;
+      m[5] = o.dest_pack;
+      m[6] = (o.door_autoclose ? 1 : 0) | (o.crashed ? 2 : 0);
+      m[7] = o.done_mask;
+      m[8] = e.hdr()[H_STEP];
+      m[9] = e.hdr()[H_EPISODE];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// kernels: one wave per env, MFG_WPB waves per workgroup, the env record image in dynamic LDS
+// ------------------------------------------------------------------------------------------------
+#define MFG_WPB 4
+
+__device__ __forceinline__ bool wave_env(const MfgDevSpec* S, uint8_t* smem, long long B, Env& e, long long& env) {
+  const int wid = threadIdx.x >> 6;
+  env = (long long)blockIdx.x * MFG_WPB + wid;
+  e.S = S;
+  e.lds = smem + (size_t)wid * S->lds_per_wave;
+  e.lane = lane_id();
+  return env < B;
+}
+
+// creation (init=1): random.seed(py_seed), Factory.__init__ (floor list, OBSBuilder shuffle); then reset
+template <int MAXPTS, typename OT>
+__global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S, uint8_t* state, long long B,
+                                                        const uint8_t* mask, OT* obs, int init,
+                                                        unsigned long long seed_base) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  Env e;
+  long long env;
+  if (!wave_env(S, smem, B, e, env)) return;
+  if (mask && !mask[env]) return;
+  uint8_t* rec = state + (size_t)env * S->L.size;
+  int* scratch = (int*)(e.lds + S->L.size);
+  if (init) {
+    for (int i = e.lane; i < (S->L.size >> 2); i += MFG_WAVE) ((int*)e.lds)[i] = 0;
+    wave_sync();
+    const unsigned long long py_seed = seed_base + (unsigned long long)env;
+    uint32_t key[2] = {(uint32_t)py_seed, (uint32_t)(py_seed >> 32)};
+    mt_seed(e, key, key[1] ? 2 : 1);
+    for (int i = e.lane; i < S->nf; i += MFG_WAVE) e.perm()[i] = (uint16_t)S->floor_init[i];
+    if (e.lane == 0) {
+      e.pcg()[0] = S->pcg_init_hi; e.pcg()[1] = S->pcg_init_lo;
+      e.pcg()[2] = S->pcg_inc_hi;  e.pcg()[3] = S->pcg_inc_lo;
+    }
+    if (e.lane < S->nd) e.door()[e.lane] = DW_PRESENT;
+    for (int r = 0; r < S->s.n_rules; r++) {
+      const mfg_rule& ru = S->s.rules[r];
+      if (e.lane == 0 && ru.op == MFG_RULE_RESPAWN_ITEMS) e.rctr()[r] = ru.i[1];
+      if (e.lane == 0 && ru.op == MFG_RULE_RESPAWN_DIRT) e.rctr()[r] = ru.i[0];
+    }
+    e.setH(H_EPISODE, -1);
+    wave_sync();
+    floor_shuffle(e);  // OBSBuilder.__init__: `for pos in state.entities.floorlist` (observation_builder.py:57)
+  } else {
+    rec_load(e, rec);
+  }
+  env_reset(e, scratch);
+  if (obs) build_obs<MAXPTS, OT>(e, obs + (size_t)env * S->A * S->obs_agent_stride);
+  else e.setH(H_OBS_INIT, 1);
+  rec_store(e, rec);
+}
+
+template <int MAXPTS, typename OT>
+__global__ void __launch_bounds__(MFG_WPB * 64) k_step(const MfgDevSpec* S, uint8_t* state, long long B, int K,
+                                                       const int32_t* actions, unsigned philox_seed,
+                                                       unsigned env_base, long long step_base, double* reward, uint8_t* done, OT* obs,
+                                                       uint8_t* ev_act, uint8_t* ev_watch, int32_t* ev_misc,
+                                                       int auto_reset) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  Env e;
+  long long env;
+  if (!wave_env(S, smem, B, e, env)) return;
+  uint8_t* rec = state + (size_t)env * S->L.size;
+  int* scratch = (int*)(e.lds + S->L.size);
+  const int A = S->A;
+  rec_load(e, rec);
+  for (int k = 0; k < K; k++) {
+    const size_t row = (size_t)k * B + env;
+    int my_act = 0;
+    if (e.lane < A) {
+      if (actions) {
+        my_act = actions[row * A + e.lane];
+      } else {
+        const uint32_t u = philox_u32(philox_seed, env_base + (uint32_t)env, (uint32_t)(step_base + k),
+                                    (uint32_t)e.lane);
+        my_act = (int)(((uint64_t)u * (uint64_t)S->s.n_actions[e.lane]) >> 32);
+      }
+    }
+    StepOut o;
+    env_step(e, my_act, o, scratch);
+    write_step_outputs(e, o, row, reward, done, ev_act, ev_watch, ev_misc);
+    if (o.done && auto_reset) env_reset(e, scratch);
+    if (obs) build_obs<MAXPTS, OT>(e, obs + row * A * S->obs_agent_stride);
+  }
+  rec_store(e, rec);
+}
+
+// ================================================================================================
+// host side: C-ABI (include/mfg.h)
+// ================================================================================================
+struct mfg_engine {
+  int device = 0;
+  long long B = 0;
+  MfgDevSpec h{};
+  MfgDevSpec* d_spec = nullptr;
+  std::vector<void*> d_bufs;
+  uint8_t* d_state = nullptr;
+  int maxpts = 0;
+};
+
+static thread_local std::string g_err;
+static int fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+#define HIPCHK(x)                                                               \
+  do {                                                                          \
+    hipError_t _e = (x);                                                        \
+    if (_e != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+extern "C" const char* mfg_last_error(void) { return g_err.c_str(); }
+
+template <typename T>
+static int upload(mfg_engine* e, const T* src, size_t n, const T** dst) {
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, sizeof(T) * (n ? n : 1)));
+  if (n) HIPCHK(hipMemcpy(p, src, sizeof(T) * n, hipMemcpyHostToDevice));
+  e->d_bufs.push_back(p);
+  *dst = (const T*)p;
+  return 0;
+}
+
+// numpy SeedSequence(entropy) -> PCG64 initial state (numpy/random/bit_generator.pyx, pcg64.h)
+static void pcg64_seed(uint32_t entropy, uint64_t* st_hi, uint64_t* st_lo, uint64_t* inc_hi, uint64_t* inc_lo) {
+  auto hashmix = [](uint32_t v, uint32_t& hc) {
+    v ^= hc; hc *= 0x931e8875u; v *= hc; v ^= v >> 16; return v;
+  };
+  auto mix = [](uint32_t x, uint32_t y) {
+    uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y; r ^= r >> 16; return r;
+  };
+  uint32_t pool[4], hc = 0x43b0d7e5u;
+  pool[0] = hashmix(entropy, hc);
+  for (int i = 1; i < 4; i++) pool[i] = hashmix(0u, hc);
+  for (int s = 0; s < 4; s++)
+    for (int d = 0; d < 4; d++)
+      if (s != d) pool[d] = mix(pool[d], hashmix(pool[s], hc));
+  uint32_t st[8], hb = 0x8b51f9ddu;
+  for (int i = 0; i < 8; i++) {
+    uint32_t v = pool[i % 4];
+    v ^= hb; hb *= 0x58f38dedu; v *= hb; v ^= v >> 16;
+    st[i] = v;
+  }
+  uint64_t w[4];
+  for (int i = 0; i < 4; i++) w[i] = (uint64_t)st[2 * i] | ((uint64_t)st[2 * i + 1] << 32);
+  typedef unsigned __int128 u128;
+  const u128 mult = ((u128)2549297995355413924ULL << 64) | 4865540595714422341ULL;
+  u128 seed = ((u128)w[0] << 64) | w[1], inc = ((((u128)w[2] << 64) | w[3]) << 1) | 1u;
+  u128 state = 0;
+  state = state * mult + inc;
+  state += seed;
+  state = state * mult + inc;
+  *st_hi = (uint64_t)(state >> 64); *st_lo = (uint64_t)state;
+  *inc_hi = (uint64_t)(inc >> 64); *inc_lo = (uint64_t)inc;
+}
+
+static int align_up(int x, int a) { return (x + a - 1) / a * a; }
+
+static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int dropmax, int destmax) {
+  int o = 0;
+  const int A = s->n_agents, nd = s->n_doors;
+  const int dm = s->has_dirt ? MFG_DIRT_MAX : 0;
+  L->o_hdr = o; o += 4 * MFG_HDR_N;
+  L->o_rule_ctr = o; o += 4 * MFG_MAX_RULES;
+  L->o_agent_pos = o; o += 4 * A;
+  L->o_agent_arr = o; o += 4 * A;
+  L->o_agent_par = o; o += 4 * A;
+  L->o_frozen_org = o; o += 4 * A;
+  L->o_frozen_gp = o; o += 4 * A;
+  L->o_door = o; o += 4 * nd;
+  L->o_items = o; o += 4 * imax;
+  L->o_pods = o; o += 4 * pmax;
+  L->o_drops = o; o += 4 * dropmax;
+  L->o_dests = o; o += 4 * destmax;
+  L->o_dirt_pos = o; o += 4 * dm;
+  L->o_dirt_id = o; o += 4 * dm;
+  o = align_up(o, 8);
+  L->o_battery = o; o += 8 * A;
+  L->o_frozen_bat = o; o += 8 * A;
+  L->o_dirt_amt = o; o += 8 * dm;
+  L->o_pcg = o; o += 8 * 4;
+  L->o_mt = o; o += 4 * 624;
+  L->o_perm = o; o += 2 * s->n_floor;
+  L->size = align_up(o, 16);
+}
+
+extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out) {
+  if (!s || !out) return fail("null argument");
+  if (s->abi_version != MFG_ABI_VERSION) return fail("spec ABI version mismatch");
+  if (s->n_agents < 1 || s->n_agents > MFG_MAX_AGENTS) return fail("n_agents out of range");
+  if (s->n_doors > MFG_MAX_DOORS) return fail("too many doors");
+  if (s->pomdp_r < 1 || s->pomdp_r > 3) return fail("engine supports pomdp_r in [1,3] (window d*d <= 64 lanes)");
+  if (s->H * s->W > 65535) return fail("level too large for 16-bit cell indices");
+  if (s->has_machines || s->has_maintainers) return fail("machines/maintainers are not implemented on the device");
+  auto* e = new mfg_engine();
+  e->device = device;
+  e->B = n_envs;
+  if (hipSetDevice(device) != hipSuccess) { delete e; return fail("hipSetDevice failed"); }
+  MfgDevSpec& h = e->h;
+  h.s = *s;
+  const int HW = s->H * s->W;
+  h.HW = HW; h.nf = s->n_floor; h.nw = s->n_walls; h.nd = s->n_doors; h.A = s->n_agents;
+  h.r = s->pomdp_r; h.d = 2 * s->pomdp_r + 1; h.dd = h.d * h.d; h.nrays = s->n_rays;
+  if (h.nrays > 64) { delete e; return fail("more than 64 rays"); }
+  h.maxpts = 2 * s->pomdp_r + 2;
+  int lmax = 1;
+  for (int a = 0; a < s->n_agents; a++) lmax = s->n_layers[a] > lmax ? s->n_layers[a] : lmax;
+  h.lmax = lmax;
+  h.obs_agent_stride = lmax * h.dd;
+  int imax = 0, pmax = 0, dropmax = 0, destmax = 0;
+  for (int r = 0; r < s->n_rules; r++) {
+    const mfg_rule& ru = s->rules[r];
+    if (ru.op == MFG_RULE_SPAWN_ITEMS) imax = ru.i[0];
+    if (ru.op == MFG_RULE_SPAWN_PODS) pmax = ru.i[0];
+    if (ru.op == MFG_RULE_SPAWN_DROPOFFS) dropmax = ru.i[0];
+    if (ru.op == MFG_RULE_SPAWN_DESTS) destmax = ru.i[0];
+  }
+  if (imax > 64 || pmax > 64 || dropmax > 64 || destmax > 64) { delete e; return fail("group quantity > 64"); }
+  h.imax = imax; h.pmax = pmax; h.dropmax = dropmax; h.destmax = destmax;
+  make_layout(s, &h.L, imax, pmax, dropmax, destmax);
+  h.lds_per_wave = align_up(h.L.size + 4 * 64, 16);
+  pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
+  // static tables
+  std::vector<uint8_t> door_of(HW, 0xFF);
+  for (int d = 0; d < s->n_doors; d++) door_of[s->door_cells[d]] = (uint8_t)d;
+  std::vector<int8_t> rp((size_t)h.nrays * h.maxpts * 2, 0);
+  std::vector<uint8_t> rlen(h.nrays);
+  for (int r = 0; r < h.nrays; r++) {
+    const int p0 = s->ray_off[r], p1 = s->ray_off[r + 1];
+    if (p1 - p0 > h.maxpts) { delete e; return fail("ray longer than 2r+2 points"); }
+    rlen[r] = (uint8_t)(p1 - p0);
+    for (int p = p0; p < p1; p++) {
+      rp[((size_t)r * h.maxpts + (p - p0)) * 2] = (int8_t)s->ray_pts[2 * p];
+      rp[((size_t)r * h.maxpts + (p - p0)) * 2 + 1] = (int8_t)s->ray_pts[2 * p + 1];
+    }
+  }
+  int rc = 0;
+  rc |= upload(e, s->level, HW, &h.level);
+  rc |= upload(e, door_of.data(), HW, &h.door_of);
+  rc |= upload(e, s->wall_cells, s->n_walls, &h.wall_cells);
+  rc |= upload(e, s->door_cells, s->n_doors, &h.door_cells);
+  rc |= upload(e, s->floor_cells, s->n_floor, &h.floor_init);
+  rc |= upload(e, rp.data(), rp.size(), &h.ray_pts);
+  rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
+  if (rc) { delete e; return -1; }
+  if (hipMalloc((void**)&e->d_spec, sizeof(MfgDevSpec)) != hipSuccess ||
+      hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
+    delete e; return fail("spec upload failed");
+  }
+  if (hipMalloc((void**)&e->d_state, (size_t)h.L.size * (size_t)n_envs) != hipSuccess) {
+    delete e; return fail("state allocation failed");
+  }
+  e->maxpts = h.maxpts;
+  *out = e;
+  return 0;
+}
+
+extern "C" int mfg_destroy(mfg_engine* e) {
+  if (!e) return 0;
+  (void)hipSetDevice(e->device);
+  for (void* p : e->d_bufs) (void)hipFree(p);
+  if (e->d_spec) (void)hipFree(e->d_spec);
+  if (e->d_state) (void)hipFree(e->d_state);
+  delete e;
+  return 0;
+}
+
+// record layout for host-side decoding (tests, snapshots): [size, o_hdr, ..., o_perm, lmax, obs_agent_stride]
+extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
+  const MfgLayout& L = e->h.L;
+  const int32_t v[] = {L.size, L.o_hdr, L.o_rule_ctr, L.o_agent_pos, L.o_agent_arr, L.o_agent_par, L.o_frozen_org,
+                       L.o_frozen_gp, L.o_door, L.o_items, L.o_pods, L.o_drops, L.o_dests, L.o_dirt_pos,
+                       L.o_dirt_id, L.o_battery, L.o_frozen_bat, L.o_dirt_amt, L.o_pcg, L.o_mt, L.o_perm,
+                       e->h.lmax, e->h.obs_agent_stride, e->h.lds_per_wave};
+  const int n = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n; i++) out[i] = v[i];
+  return n;
+}
+
+extern "C" void* mfg_state_ptr(mfg_engine* e) { return e ? e->d_state : nullptr; }
+
+template <int MP, typename OT>
+static hipError_t launch_reset_t(mfg_engine* e, const uint8_t* mask, OT* obs, int init, unsigned long long seed_base,
+                                 hipStream_t st) {
+  const unsigned grid = (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB);
+  const size_t lds = (size_t)e->h.lds_per_wave * MFG_WPB;
+  hipLaunchKernelGGL((k_reset<MP, OT>), dim3(grid), dim3(MFG_WPB * 64), lds, st, e->d_spec, e->d_state,
+                     (long long)e->B, mask, obs, init, seed_base);
+  return hipGetLastError();
+}
+template <int MP, typename OT>
+static hipError_t launch_step_t(mfg_engine* e, int K, const int32_t* actions, unsigned seed, unsigned env_base,
+                                long long step_base, double* reward, uint8_t* done, OT* obs, uint8_t* ev_act,
+                                uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, hipStream_t st) {
+  const unsigned grid = (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB);
+  const size_t lds = (size_t)e->h.lds_per_wave * MFG_WPB;
+  hipLaunchKernelGGL((k_step<MP, OT>), dim3(grid), dim3(MFG_WPB * 64), lds, st, e->d_spec, e->d_state,
+                     (long long)e->B, K, actions, seed, env_base, step_base, reward, done, obs, ev_act, ev_watch,
+                     ev_misc, auto_reset);
+  return hipGetLastError();
+}
+
+#define DISPATCH_MP(MPVAL, CALL) \
+  switch (MPVAL) {               \
+    case 4: { constexpr int MP = 4; CALL; } break; \
+    case 6: { constexpr int MP = 6; CALL; } break; \
+    case 8: { constexpr int MP = 8; CALL; } break; \
+    default: return fail("unsupported ray length"); \
+  }
+
+// reset (init=1: create envs, seeding env i with random.seed(seed_base + i)); obs_dtype 0=f32 1=f64
+extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init,
+                         uint64_t seed_base, void* stream) {
+  if (!e) return fail("null engine");
+  hipError_t err = hipSuccess;
+  hipStream_t st = (hipStream_t)stream;
+  if (obs_dtype == 1) {
+    DISPATCH_MP(e->maxpts, err = (launch_reset_t<MP, double>(e, mask, (double*)obs, init, seed_base, st)));
+  } else {
+    DISPATCH_MP(e->maxpts, err = (launch_reset_t<MP, float>(e, mask, (float*)obs, init, seed_base, st)));
+  }
+  if (err != hipSuccess) return fail(std::string("k_reset launch: ") + hipGetErrorString(err));
+  return 0;
+}
+
+// K fused steps. actions: device [K][B][A] int32, or NULL -> Philox4x32-10 synthetic actions keyed
+// (philox_seed, env_base+env) at counter (step_base+k, agent). Outputs (each may be NULL):
+// reward [K][B][A] f64, done [K][B] u8, obs [K][B][A][lmax][d][d], ev_act/ev_watch [K][B][A] u8,
+// ev_misc [K][B][10] i32. auto_reset: envs that finish are reset in-kernel (the obs row is then the
+// first observation of the new episode).
+extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
+                        int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype,
+                        uint8_t* ev_act, uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
+  if (!e) return fail("null engine");
+  if (K < 1) return fail("K must be >= 1");
+  hipError_t err = hipSuccess;
+  hipStream_t st = (hipStream_t)stream;
+  if (obs_dtype == 1) {
+    DISPATCH_MP(e->maxpts, err = (launch_step_t<MP, double>(e, K, actions, philox_seed, env_base, step_base, reward,
+                                                            done, (double*)obs, ev_act, ev_watch, ev_misc,
+                                                            auto_reset, st)));
+  } else {
+    DISPATCH_MP(e->maxpts, err = (launch_step_t<MP, float>(e, K, actions, philox_seed, env_base, step_base, reward,
+                                                           done, (float*)obs, ev_act, ev_watch, ev_misc, auto_reset,
+                                                           st)));
+  }
+  if (err != hipSuccess) return fail(std::string("k_step launch: ") + hipGetErrorString(err));
+  return 0;
+}
+
+// snapshots (checkpoints == fixtures): whole state buffer device<->device, B * layout.size bytes
+extern "C" int mfg_export_state(mfg_engine* e, void* dst, void* stream) {
+  if (!e || !dst) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(dst, e->d_state, (size_t)e->h.L.size * e->B, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mfg_import_state(mfg_engine* e, const void* src, void* stream) {
+  if (!e || !src) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(e->d_state, src, (size_t)e->h.L.size * e->B, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int64_t mfg_state_bytes(const mfg_engine* e) { return e ? (int64_t)e->h.L.size * e->B : -1; }
+extern "C" int mfg_abi_version(void) { return MFG_ABI_VERSION; }

@@ -1,0 +1,192 @@
+"""ctypes binding of the HIP engine (libmfg_hip.so, C-ABI in include/mfg.h).
+
+The product path is the HIP library: there is no CPU fallback. If the library is missing or no GPU is
+visible the constructor raises. Device memory for inputs/outputs is owned by the caller (torch tensors);
+the engine owns the per-env state records.
+"""
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import abi
+
+LIB_PATH = Path(__file__).resolve().parent / '_lib' / 'libmfg_hip.so'
+EV_MISC = 10
+
+LAYOUT_KEYS = ['size', 'o_hdr', 'o_rule_ctr', 'o_agent_pos', 'o_agent_arr', 'o_agent_par', 'o_frozen_org',
+               'o_frozen_gp', 'o_door', 'o_items', 'o_pods', 'o_drops', 'o_dests', 'o_dirt_pos', 'o_dirt_id',
+               'o_battery', 'o_frozen_bat', 'o_dirt_amt', 'o_pcg', 'o_mt', 'o_perm', 'lmax', 'obs_agent_stride',
+               'lds_per_wave']
+# header slots (csrc/mfg_device.h)
+HDR = {k: i for i, k in enumerate([
+    'step', 'episode', 'crashed', 'frozen', 'obs_init', 'debt', 'mt_idx', 'n_items', 'n_pods', 'n_drops',
+    'n_dirt', 'n_dests', 'item_base', 'pod_base', 'drop_base', 'dest_base', 'bat_base', 'arrival', 'done',
+    'overflow', 'cnt_agent', 'cnt_battery', 'cnt_pod', 'cnt_drop', 'cnt_item', 'cnt_dirt', 'cnt_dest',
+    'cnt_machine', 'cnt_maint', 'cnt_gp', 'total_steps'])}
+
+_lib = None
+
+
+def load_lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f'HIP engine library missing: {LIB_PATH} (run __graft_entry__.build())')
+    L = C.CDLL(str(LIB_PATH))
+    L.mfg_create.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_void_p)]
+    L.mfg_create.restype = C.c_int
+    L.mfg_destroy.argtypes = [C.c_void_p]
+    L.mfg_destroy.restype = C.c_int
+    L.mfg_last_error.restype = C.c_char_p
+    L.mfg_layout.argtypes = [C.c_void_p, C.c_void_p]
+    L.mfg_layout.restype = C.c_int
+    L.mfg_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_void_p]
+    L.mfg_reset.restype = C.c_int
+    L.mfg_step.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int64, C.c_void_p,
+                           C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                           C.c_void_p]
+    L.mfg_step.restype = C.c_int
+    L.mfg_export_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mfg_export_state.restype = C.c_int
+    L.mfg_import_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mfg_import_state.restype = C.c_int
+    L.mfg_state_bytes.argtypes = [C.c_void_p]
+    L.mfg_state_bytes.restype = C.c_int64
+    L.mfg_abi_version.restype = C.c_int
+    if L.mfg_abi_version() != 1:
+        raise RuntimeError('libmfg_hip.so ABI version mismatch')
+    _lib = L
+    return L
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f'{what} failed: {load_lib().mfg_last_error().decode()}')
+
+
+class Engine:
+    """B environments of one compiled spec on one GPU."""
+
+    def __init__(self, spec, n_envs, device=0):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError('mfg_amd.Engine needs a GPU (HIP); no CPU fallback exists')
+        self.torch = torch
+        self.L = load_lib()
+        self.spec = spec
+        self.B = int(n_envs)
+        self.device = torch.device('cuda', device)
+        torch.cuda.set_device(self.device)
+        h = C.c_void_p()
+        _check(self.L.mfg_create(C.byref(spec.c), device, self.B, C.byref(h)), 'mfg_create')
+        self.h = h
+        lay = np.zeros(64, np.int32)
+        n = self.L.mfg_layout(self.h, lay.ctypes.data_as(C.c_void_p))
+        self.layout = dict(zip(LAYOUT_KEYS, [int(x) for x in lay[:n]]))
+        self.lmax = self.layout['lmax']
+        self.A = spec.n_agents
+        self.d = spec.d
+
+    def close(self):
+        if getattr(self, 'h', None) is not None and self.h.value:
+            self.L.mfg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def obs_shape(self, K=None):
+        s = (self.B, self.A, self.lmax, self.d, self.d)
+        return s if K is None else (K,) + s
+
+    def reset(self, obs=None, mask=None, init=False, seed_base=0):
+        dt = 1 if (obs is not None and obs.dtype == self.torch.float64) else 0
+        _check(self.L.mfg_reset(self.h, _ptr(mask), _ptr(obs), dt, int(init), int(seed_base), self._stream()),
+               'mfg_reset')
+
+    def step(self, K=1, actions=None, philox_seed=0, env_base=0, step_base=0, reward=None, done=None, obs=None,
+             ev_act=None, ev_watch=None, ev_misc=None, auto_reset=True):
+        dt = 1 if (obs is not None and obs.dtype == self.torch.float64) else 0
+        _check(self.L.mfg_step(self.h, int(K), _ptr(actions), int(philox_seed) & 0xFFFFFFFF, int(env_base),
+                               int(step_base), _ptr(reward), _ptr(done), _ptr(obs), dt, _ptr(ev_act),
+                               _ptr(ev_watch), _ptr(ev_misc), int(bool(auto_reset)), self._stream()), 'mfg_step')
+
+    def export_state(self):
+        t = self.torch.empty((self.B, self.layout['size']), dtype=self.torch.uint8, device=self.device)
+        _check(self.L.mfg_export_state(self.h, _ptr(t), self._stream()), 'mfg_export_state')
+        return t
+
+    def import_state(self, t):
+        assert t.dtype == self.torch.uint8 and t.numel() == self.B * self.layout['size']
+        _check(self.L.mfg_import_state(self.h, _ptr(t.contiguous()), self._stream()), 'mfg_import_state')
+
+
+class RecordView:
+    """Host-side decoder of one env state record (numpy bytes), using the engine's layout."""
+
+    def __init__(self, rec: np.ndarray, layout, spec):
+        self.b = rec.tobytes() if isinstance(rec, np.ndarray) else bytes(rec)
+        self.L = layout
+        self.spec = spec
+
+    def i32(self, off, n):
+        return np.frombuffer(self.b, np.int32, n, off)
+
+    def f64(self, off, n):
+        return np.frombuffer(self.b, np.float64, n, off)
+
+    def hdr(self, k):
+        return int(self.i32(self.L['o_hdr'], 32)[HDR[k]])
+
+    def agent_pos(self):
+        return self.i32(self.L['o_agent_pos'], self.spec.n_agents)
+
+    def battery(self):
+        return self.f64(self.L['o_battery'], self.spec.n_agents)
+
+    def doors(self):
+        w = self.i32(self.L['o_door'], self.spec.c.n_doors)
+        return (w & 1), ((w >> 8) & 0xFF), ((w >> 16) & 1)
+
+    def group(self, name):
+        off, hn = {'items': ('o_items', 'n_items'), 'pods': ('o_pods', 'n_pods'), 'drops': ('o_drops', 'n_drops'),
+                   'dests': ('o_dests', 'n_dests'), 'dirt': ('o_dirt_pos', 'n_dirt')}[name]
+        return self.i32(self.L[off], self.hdr(hn))
+
+    def dirt(self):
+        n = self.hdr('n_dirt')
+        return self.i32(self.L['o_dirt_pos'], n), self.i32(self.L['o_dirt_id'], n), self.f64(self.L['o_dirt_amt'], n)
+
+    def mt(self):
+        st = np.frombuffer(self.b, np.uint32, 624, self.L['o_mt']).copy()
+        return np.concatenate([st, np.asarray([self.hdr('mt_idx')], np.uint32)])
+
+    def perm(self):
+        return np.frombuffer(self.b, np.uint16, self.spec.c.n_floor, self.L['o_perm']).astype(np.int32)
+
+    def pcg(self):
+        return np.frombuffer(self.b, np.uint64, 4, self.L['o_pcg'])
+
+
+def events_from_rows(ev_act, ev_watch, ev_misc):
+    """One env-step's device event rows -> dict in the MfgEvents layout used by info.rebuild_info."""
+    m = [int(x) for x in ev_misc]
+    dest = [((m[5] >> (8 * k)) & 0xFF) - 1 for k in range(4)]
+    return dict(act=[int(x) for x in ev_act], watch=[int(x) for x in ev_watch],
+                door_coll=(m[0] & 0xFFFFFFFF) | ((m[1] & 0xFFFFFFFF) << 32), maint_coll=0,
+                respawn_items_value=m[2], dirt_spawn_value=m[3], dirt_spawn_valid=m[4],
+                dest_reach_agent=dest, door_autoclose=m[6] & 1, crashed=(m[6] >> 1) & 1, done_mask=m[7],
+                step=m[8])
