@@ -175,9 +175,43 @@ typedef struct mfg_events {
 /* ---- engine ABI (HIP) ---- */
 typedef struct mfg_engine mfg_engine;
 
+/* ABI version of the loaded library (== MFG_ABI_VERSION). */
+int mfg_abi_version(void);
+
+/* Create B = n_envs environments of `spec` on HIP device `device`. Replaces Factory.__init__
+ * (factory.py:81-129) for a whole batch; no env is initialised until mfg_reset(init=1). */
 int mfg_create(const mfg_spec* spec, int device, int64_t n_envs, mfg_engine** out);
 int mfg_destroy(mfg_engine* e);
 const char* mfg_last_error(void);
+
+/* Reset envs (mask[b] != 0, or all if mask == NULL); Factory.reset (factory.py:134-148).
+ * init = 1 additionally creates the envs: env b is seeded like `random.seed(seed_base + b)` before
+ * `Factory(cfg)` (SURVEY §8c seeding contract). obs (device, may be NULL): [B][A][lmax][d][d],
+ * obs_dtype 0 = float32, 1 = float64. */
+int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init, uint64_t seed_base,
+              void* stream);
+
+/* K fused env-steps of every env; Factory.step (factory.py:189-220) + auto-reset.
+ * actions: device int32 [K][B][A] indices into each agent's action list, or NULL for synthetic uniform
+ * actions from Philox4x32-10 keyed (philox_seed, env_base + b) at counter (step_base + k, agent).
+ * Outputs (device, each may be NULL): reward f64 [K][B][A], done u8 [K][B], obs [K][B][A][lmax][d][d],
+ * ev_act / ev_watch u8 [K][B][A] and ev_misc i32 [K][B][10] (the info-dict event record).
+ * auto_reset != 0: an env whose step is done is reset in the same launch; its obs row is then the new
+ * episode's first observation. Pending floor-shuffle debt is replayed (mfg_replay) before returning. */
+int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
+             int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
+             uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream);
+
+/* Replay pending membership-only floor shuffles (check_pos_validity, states.py:259-270, Q3). */
+int mfg_replay(mfg_engine* e, void* stream);
+
+/* Per-env state record layout (offsets) for host-side decoding; returns the number of ints written. */
+int mfg_layout(const mfg_engine* e, int32_t* out);
+void* mfg_state_ptr(mfg_engine* e);
+int64_t mfg_state_bytes(const mfg_engine* e);
+/* Snapshots (checkpoint / resume, parity fixtures): whole state buffer device <-> device. */
+int mfg_export_state(mfg_engine* e, void* dst, void* stream);
+int mfg_import_state(mfg_engine* e, const void* src, void* stream);
 
 #ifdef __cplusplus
 }

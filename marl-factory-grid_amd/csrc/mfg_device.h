@@ -72,7 +72,11 @@ struct MfgDevSpec {
   const int32_t* floor_init; // [nf]
   const int8_t* ray_pts;     // [nrays][maxpts][2] (dx, dy), padded
   const uint8_t* ray_len;    // [nrays]
+  const uint32_t* wall_bits; // [(HW+31)/32] static light/position blockers (walls)
+  int32_t n_wd_pairs;        // static identifier collisions Wall[k]/Door[k] that one ray fan can reach
+  const int32_t* wd_pairs;   // [n_wd_pairs][3]: k, wall cell, door cell
   uint64_t pcg_init_hi, pcg_init_lo, pcg_inc_hi, pcg_inc_lo;  // default_rng(env_seed) state after seeding
   MfgLayout L;
-  int32_t lds_per_wave;      // bytes of dynamic LDS per wave
+  int32_t lds_per_wave;      // bytes of dynamic LDS per wave (k_step / k_reset)
+  int32_t lds_replay_per_wave, replay_jtab_off;  // k_replay slice: [hdr][MT + perm][jtab]
 };

@@ -31,6 +31,12 @@ __device__ __forceinline__ u64 lt_mask() { return (1ull << lane_id()) - 1ull; }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double rld(double v, int l) {
+  const unsigned long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 __device__ __forceinline__ u64 wave_or64(u64 v) {
   unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
 #pragma unroll
@@ -46,9 +52,13 @@ __device__ __forceinline__ u64 wave_or64(u64 v) {
 // ------------------------------------------------------------------------------------------------
 struct Env {
   const MfgDevSpec* S;
-  uint8_t* lds;  // this wave's LDS slice == image of the HBM record
+  uint8_t* lds;     // this wave's LDS slice == image of the HBM record
+  int* scratch;     // 512 ints after the record (spawn positions, id-collision pairs)
+  uint32_t* jtab;   // [nf + 1] tagged max-table for the parallel shuffle blocks (not persisted)
+  uint32_t* light;  // [(HW+31)/32] light-blocking bitmap for the ray walk (rebuilt per render)
+  int* hdrp;        // header slots (inside the record image, or a separate slice in k_replay)
   int lane;
-  __device__ int* hdr() const { return (int*)(lds + S->L.o_hdr); }
+  __device__ int* hdr() const { return hdrp; }
   __device__ int* rctr() const { return (int*)(lds + S->L.o_rule_ctr); }
   __device__ int* agpos() const { return (int*)(lds + S->L.o_agent_pos); }
   __device__ int* agarr() const { return (int*)(lds + S->L.o_agent_arr); }
@@ -111,26 +121,42 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
   return c ^ (y >> 1) ^ ((y & 1u) ? MT_MATRIX : 0u);
 }
-// In-place twist in three dependency phases; within a wave every LDS read of an iteration is issued
-// before its writes, and later iterations only read indices no earlier iteration has written.
+// In-place twist in its three dependency phases (i<227: old inputs; 227<=i<454: mt[i-227] new;
+// 454<=i<623: mt[i-227] new). Each phase issues all its LDS reads before any of its writes, so one
+// wave pays three LDS round trips per 624 draws.
 __device__ void mt_twist(const Env& e) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
-  for (int b = 0; b < 227; b += MFG_WAVE) {
-    int i = b + lane;
-    uint32_t v = 0;
-    if (i < 227) v = mt_mix(mt[i], mt[i + 1], mt[i + 397]);
-    wave_sync();
-    if (i < 227) mt[i] = v;
-    wave_sync();
+  uint32_t v[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int i = t * MFG_WAVE + lane;
+    v[t] = i < 227 ? mt_mix(mt[i], mt[i + 1], mt[i + 397]) : 0u;
   }
-  for (int b = 227; b < 623; b += MFG_WAVE) {
-    int i = b + lane;
-    uint32_t v = 0;
-    if (i < 623) v = mt_mix(mt[i], mt[i + 1], mt[i - 227]);
-    wave_sync();
-    if (i < 623) mt[i] = v;
-    wave_sync();
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int i = t * MFG_WAVE + lane;
+    if (i < 227) mt[i] = v[t];
+  }
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int i = 227 + t * MFG_WAVE + lane;
+    v[t] = i < 454 ? mt_mix(mt[i], mt[i + 1], mt[i - 227]) : 0u;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int i = 227 + t * MFG_WAVE + lane;
+    if (i < 454) mt[i] = v[t];
+  }
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    const int i = 454 + t * MFG_WAVE + lane;
+    v[t] = i < 623 ? mt_mix(mt[i], mt[i + 1], mt[i - 227]) : 0u;
+  }
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    const int i = 454 + t * MFG_WAVE + lane;
+    if (i < 623) mt[i] = v[t];
   }
   if (lane == 0) mt[623] = mt_mix(mt[623], mt[0], mt[396]);
   wave_sync();
@@ -141,7 +167,14 @@ __device__ void mt_twist(const Env& e) {
 // parallel; which draws are accepted (and for which i) is the fixed point of
 //   A_l = #accepted lanes < l,  i_l = icur - A_l,  accept_l = (y_l >> (32 - bitlen(i_l+1))) <= i_l,
 // found by Jacobi iteration with ballots (lane 0 is exact after 1 round, lane l after l+1; typical 2-3).
-// If perm != null the Fisher-Yates swaps are applied in order (the only serial part).
+//
+// If perm != null the accepted draws' Fisher-Yates swaps (i_t, j_t), t = accepted-lane order, are
+// applied as ONE parallel block instead of a serial chain. With i_t consecutive and j_t <= i_t:
+//   V_t (value leaving i_t) = V_{pi(t)} if pi(t) = last s<t with j_s == i_t exists, else P0[i_t]
+//   F_t (value landing on i_t) = V_{pj(t)} if pj(t) = last s<t with j_s == j_t exists, else P0[j_t]
+// (P0 = block-start values). pi comes from a tagged LDS max-table keyed by position (only s<t can have
+// j_s == i_t); pj from a loop over the few lanes that have a later equal j; V by pointer jumping.
+// Writes: perm[i_t] = F_t; perm[j_t] = V_t unless a later lane rewrites j_t or j_t is a later i.
 // Returns j of the first accepted draw (i == hi), used by empty_positions().pop().
 __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
   uint32_t* mt = e.mt();
@@ -177,22 +210,45 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
     const int consumed = popc(ballot(act));
     const int nacc = popc(accm);
     if (first_j < 0 && nacc) first_j = rl((int)r, ffs64(accm));
-    if (perm) {
-      // serial Fisher-Yates swaps for the accepted draws, in draw order
-      const int ri = (int)r;
-      if (lane == 0) {
-        u64 m = accm;
-        while (m) {
-          const int L = ffs64(m);
-          m &= m - 1;
-          const int i = rl(il, L), j = rl(ri, L);
-          const uint16_t a = perm[i], b = perm[j];
-          perm[i] = b;
-          perm[j] = a;
-        }
+#ifndef MFG_ABLATE_NOSWAP
+    if (perm && nacc) {
+      const int i = acc ? il : 0, j = acc ? (int)r : 0;
+      const int P0i = acc ? (int)perm[i] : 0;
+      const int P0j = acc ? (int)perm[j] : 0;
+      uint32_t* jtab = e.jtab;
+      const uint32_t ctr = jtab[e.S->nf] + 1u;  // tag: 26-bit chunk counter (table zeroed per launch)
+      const uint32_t tag = ctr << 6;
+      if (acc) atomicMax(&jtab[j], tag | (uint32_t)lane);
+      wave_sync();
+      if (lane == 0) jtab[e.S->nf] = ctr;
+      const uint32_t tj = acc ? jtab[j] : 0u, ti = acc ? jtab[i] : 0u;
+      const bool later = acc && (tj >> 6) == ctr && (int)(tj & 63u) != lane;
+      int pj = -1;
+      u64 nm = ballot(later);  // lanes with a later equal j: the only possible pj targets
+      while (nm) {
+        const int s2 = ffs64(nm);
+        nm &= nm - 1;
+        const int js = rl(j, s2);
+        if (acc && s2 < lane && js == j) pj = s2;
       }
+      // j_s == i_t only for s <= t (j_s <= i_s < i_t for s > t); s == t is the self-swap j_t == i_t,
+      // whose predecessor on position i_t is then pj(t)
+      int pi = (acc && (ti >> 6) == ctr) ? (int)(ti & 63u) : -1;
+      if (pi == lane) pi = pj;
+      int v = P0i, ptr = pi;
+      while (ballot(ptr >= 0)) {
+        const int src = ptr >= 0 ? ptr : lane;
+        const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
+        if (ptr >= 0) { v = v2; ptr = p2; }
+      }
+      const int Vj = __shfl(v, pj >= 0 ? pj : lane);
+      const int F = pj >= 0 ? Vj : P0j;
+      const int imin = rl(il, 63 - __clzll((long long)accm));
+      if (acc) perm[i] = (uint16_t)F;
+      if (acc && !later && !(j >= imin && j < i)) perm[j] = (uint16_t)v;
       wave_sync();
     }
+#endif
     icur -= nacc;
     idx += consumed;
   }
@@ -206,6 +262,10 @@ __device__ __forceinline__ void floor_shuffle(const Env& e) { mt_randbelow_seq(e
 
 // Pay the shuffle debt accumulated by membership-only floorlist calls (check_pos_validity, Q3).
 __device__ void pay_debt(const Env& e) {
+#ifdef MFG_ABLATE_NODEBT
+  e.setH(H_DEBT, 0);
+  return;
+#endif
   int debt = e.H(H_DEBT);
   for (int k = 0; k < debt; k++) floor_shuffle(e);
   e.setH(H_DEBT, 0);
@@ -928,8 +988,22 @@ __device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
   const MfgDevSpec* S = e.S;
   if (x < 0 || y < 0 || x >= S->s.H || y >= S->s.W) return false;
   const int c = x * S->s.W + y;
-  if (S->level[c] == 1) return true;
-  return present_closed_door(e, c);
+  return (e.light[c >> 5] >> (c & 31)) & 1u;
+}
+// per-env light-blocking bitmap: walls (static) | closed doors present in the global pos_dict
+__device__ void build_light(const Env& e) {
+  const MfgDevSpec* S = e.S;
+  const int nw = (S->HW + 31) >> 5;
+  for (int w = e.lane; w < nw; w += MFG_WAVE) e.light[w] = S->wall_bits[w];
+  wave_sync();
+  if (e.lane < S->nd) {
+    const int dw = e.door()[e.lane];
+    if ((dw & DW_PRESENT) && !(dw & DW_OPEN)) {
+      const int c = S->door_cells[e.lane];
+      atomicOr(&e.light[c >> 5], 1u << (c & 31));
+    }
+  }
+  wave_sync();
 }
 
 template <int MAXPTS>
@@ -950,184 +1024,241 @@ __device__ int first_visit(const RayVis<MAXPTS>& rv, int cell) {
   return L * 32 + rl(k, L);
 }
 
+// Identifier-collision candidates (Q14), agent independent, built once per render into scratch:
+// pair q = {cellA, cellB, codeA, codeB}; code = kind << 8 | slot (kind: 1 door, 3 item, 4 pod, 5 drop,
+// 6 dirt, 7 dest, 9 wall -> slot unused, the wall is identified by its cell). Returns the pair count.
+#define OBS_MAX_PAIRS 120
+__device__ int build_id_pairs(const Env& e, int* pairs) {
+  const MfgDevSpec* S = e.S;
+  const int lane = e.lane;
+  // concatenated dynamic int-id entities: items, pods, drops, dests, dirt (<= 64 in total for dedupe)
+  const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
+  const int tot = nI + nP + nR + nS + nT;
+  int kind = 0, slot = 0, w = 0, id = -1;
+  if (lane < tot) {
+    int l = lane;
+    if (l < nI) { kind = K_ITEM; slot = l; w = e.items()[l]; id = e.hdr()[H_ITEM_BASE] + l; }
+    else if ((l -= nI) < nP) { kind = K_POD; slot = l; w = e.pods()[l]; id = e.hdr()[H_POD_BASE] + l; }
+    else if ((l -= nP) < nR) { kind = K_DROP; slot = l; w = e.drops()[l]; id = e.hdr()[H_DROP_BASE] + l; }
+    else if ((l -= nR) < nS) { kind = K_DEST; slot = l; w = e.dests()[l]; id = e.hdr()[H_DEST_BASE] + l; }
+    else { l -= nS; kind = K_DIRT; slot = l; w = e.dirtpos()[l]; id = e.dirtid()[l]; }
+    if (!(w & EW_PRESENT)) id = -1;
+  }
+  const int cell = EW_POS(w);
+  const int code = (kind << 8) | slot;
+  int n = 0;
+  // wall partner
+  {
+    const bool has = id >= 0 && id < S->nw;
+    const int wc = has ? S->wall_cells[id] : 0;
+    const u64 m = ballot(has);
+    const int rank = n + popc(m & lt_mask());
+    if (has && rank < OBS_MAX_PAIRS) {
+      pairs[4 * rank] = cell; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = 9 << 8;
+    }
+    n += popc(m);
+  }
+  // door partner
+  {
+    const bool has = id >= 0 && id < S->nd && (e.door()[id < S->nd && id >= 0 ? id : 0] & DW_PRESENT);
+    const int dc = has ? S->door_cells[id] : 0;
+    const u64 m = ballot(has);
+    const int rank = n + popc(m & lt_mask());
+    if (has && rank < OBS_MAX_PAIRS) {
+      pairs[4 * rank] = cell; pairs[4 * rank + 1] = dc; pairs[4 * rank + 2] = code;
+      pairs[4 * rank + 3] = (K_DOOR << 8) | id;
+    }
+    n += popc(m);
+  }
+  // dynamic-dynamic partners (different kinds, equal identifiers): lane l pairs with every later lane
+  for (int j = 0; j < tot && j < MFG_WAVE; j++) {
+    const int idj = rl(id, j), kj = rl(kind, j), cj = rl(cell, j), codej = rl(code, j);
+    const bool has = lane < j && id >= 0 && idj == id && kj != kind;
+    const u64 m = ballot(has);
+    const int rank = n + popc(m & lt_mask());
+    if (has && rank < OBS_MAX_PAIRS) {
+      pairs[4 * rank] = cell; pairs[4 * rank + 1] = cj; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = codej;
+    }
+    n += popc(m);
+  }
+  // static Wall[k] / Door[k] pairs (host-filtered to pairs one ray fan can reach)
+  for (int q0 = 0; q0 < S->n_wd_pairs; q0 += MFG_WAVE) {
+    const int q = q0 + lane;
+    bool has = q < S->n_wd_pairs;
+    int k = 0, wc = 0, dc = 0;
+    if (has) {
+      k = S->wd_pairs[3 * q]; wc = S->wd_pairs[3 * q + 1]; dc = S->wd_pairs[3 * q + 2];
+      has = (e.door()[k] & DW_PRESENT) != 0;
+    }
+    const u64 m = ballot(has);
+    const int rank = n + popc(m & lt_mask());
+    if (has && rank < OBS_MAX_PAIRS) {
+      pairs[4 * rank] = dc; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = (K_DOOR << 8) | k;
+      pairs[4 * rank + 3] = 9 << 8;
+    }
+    n += popc(m);
+  }
+  if (n > OBS_MAX_PAIRS) e.setH(H_OVERFLOW, 1);
+  wave_sync();
+  return n < OBS_MAX_PAIRS ? n : OBS_MAX_PAIRS;
+}
+
+struct Sup {  // per-agent suppression sets from the identifier dedupe
+  u64 items, pods, drops, dests, dirt, doors;
+  u64 walls;  // window cells whose wall is suppressed (walls outside the window are never placed)
+  int ax, ay, r, d, W;
+};
+__device__ __forceinline__ void sup_add(Sup& s, int code, int cell) {
+  const int kind = code >> 8, slot = code & 0xFF;
+  const u64 bit = 1ull << (slot & 63);
+  switch (kind) {
+    case K_ITEM: s.items |= bit; break;
+    case K_POD: s.pods |= bit; break;
+    case K_DROP: s.drops |= bit; break;
+    case K_DEST: s.dests |= bit; break;
+    case K_DIRT: s.dirt |= bit; break;
+    case K_DOOR: s.doors |= bit; break;
+    default: {
+      const int px = cell / s.W - s.ax + s.r, py = cell % s.W - s.ay + s.r;
+      if (px >= 0 && py >= 0 && px < s.d && py < s.d) s.walls |= 1ull << (px * s.d + py);
+      break;
+    }
+  }
+}
+
 template <int MAXPTS, typename OT>
 __device__ void build_obs(const Env& e, OT* out_env) {
   const MfgDevSpec* S = e.S;
-  const int A = S->A, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
+  const int A = S->A, H = S->s.H, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
   const int lane = e.lane;
   const bool frozen = e.H(H_FROZEN) != 0;
+  build_light(e);
+  int* pairs = e.scratch;
+  const int npairs = build_id_pairs(e, pairs);
+  // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
+  const int agp = lane < A ? e.agpos()[lane] : -1;
+  const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
+  const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
+  const int itw = lane < nI ? e.items()[lane] : 0;
+  const int pdw = lane < nP ? e.pods()[lane] : 0;
+  const int drw = lane < nR ? e.drops()[lane] : 0;
+  const int dsw = lane < nS ? e.dests()[lane] : 0;
+  const int dtw = lane < nT ? e.dirtpos()[lane] : 0;
+  const double dta = lane < nT ? e.dirtamt()[lane] : 0.0;
+  // this lane's ray: (dx, dy) of every point, loaded once
+  const bool has_ray = lane < S->nrays;
+  const int rlen = has_ray ? S->ray_len[lane] : 0;
+  int rdx[MAXPTS], rdy[MAXPTS];
+  {
+    const int8_t* pts = S->ray_pts + (size_t)(has_ray ? lane : 0) * MAXPTS * 2;
+#pragma unroll
+    for (int p = 0; p < MAXPTS; p++) { rdx[p] = pts[2 * p]; rdy[p] = pts[2 * p + 1]; }
+  }
+  // this lane's window cell
+  const bool inwin = lane < dd;
+  const int wpx = lane / d, wpy = lane % d;
   for (int a = 0; a < A; a++) {
-    const int apos = uni(e.agpos()[a]);
+    const int apos = rl(agp, a);
     const int ax = apos / W, ay = apos % W;
-    const int org = frozen ? uni(e.forg()[a]) : apos;
+    const int org = rl(org_l, a);
     const int ox = org / W, oy = org % W;
-    // ---- ray walk: lane = ray ----
+    // ---- ray walk (lane = ray): all blocking lookups issued up front, then the walk in registers ----
     RayVis<MAXPTS> rv;
     u64 wmask = 0;
     {
-      const bool has = lane < S->nrays;
-      const int len = has ? S->ray_len[lane] : 0;
-      const int8_t* pts = S->ray_pts + (size_t)(has ? lane : 0) * MAXPTS * 2;
-      bool alive = has;
-      int rx = ox, ry = oy;
+      bool blk[MAXPTS], cut[MAXPTS];
+      int cx_[MAXPTS], cy_[MAXPTS];
+#pragma unroll
+      for (int p = 0; p < MAXPTS; p++) {
+        const int x = ox + rdx[p], y = oy + rdy[p];
+        cx_[p] = x; cy_[p] = y;
+        blk[p] = light_block(e, x, y);
+        if (p > 0 && rdx[p] != rdx[p - 1] && rdy[p] != rdy[p - 1]) {
+          // diagonal step: cut when both orthogonal neighbours block light (ray_caster.py:89-96)
+          cut[p] = light_block(e, x, oy + rdy[p - 1]) && light_block(e, ox + rdx[p - 1], y);
+        } else {
+          cut[p] = false;
+        }
+      }
+      bool alive = has_ray;
 #pragma unroll
       for (int p = 0; p < MAXPTS; p++) {
         rv.cell[p] = -1;
-        if (alive && p < len) {
-          const int x = ox + pts[2 * p], y = oy + pts[2 * p + 1];
-          const int cx = x - rx, cy = y - ry;
-          const bool hits = light_block(e, x, y);
-          const bool diag = (cx != 0 && cy != 0) ? (light_block(e, x, y - cy) && light_block(e, x - cx, y)) : false;
-          if (!diag && x >= 0 && y >= 0 && x < S->s.H && y < W) {
+        if (alive && p < rlen) {
+          const int x = cx_[p], y = cy_[p];
+          if (!cut[p] && x >= 0 && y >= 0 && x < H && y < W) {
             rv.cell[p] = x * W + y;
             const int px = x - ax + r, py = y - ay + r;
             if (px >= 0 && py >= 0 && px < d && py < d) wmask |= 1ull << (px * d + py);
           }
-          if (hits || diag) alive = false;
-          rx = x;
-          ry = y;
+          if (blk[p] || cut[p]) alive = false;
         }
       }
     }
     const u64 vis = wave_or64(wmask);
-    // ---- identifier-collision dedupe (set(visible_entities), Q14): the later first-visit loses ----
-    // candidates: int-id entities within reach of the origin whose identifier is shared with another
-    // class (walls 0..nw-1 and doors 0..nd-1 are static; dynamic groups carry their base ids).
-    u64 sup_items = 0, sup_pods = 0, sup_drops = 0, sup_dests = 0, sup_dirt = 0, sup_doors = 0;
-    int sup_walls[8];
-    int n_sup_walls = 0;
+    // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
+    Sup sup;
+    sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = sup.walls = 0;
+    sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
     {
-      const int reach = d;  // rays walk radius d = 2r+1 (Q13)
-      auto near = [&](int cell) {
-        const int x = cell / W, y = cell % W;
-        return abs(x - ox) <= reach && abs(y - oy) <= reach;
-      };
-      // (class, slot, id, cell) of present int-id entities; walls/doors handled via id ranges
-      const int nw = S->nw, ndr = S->nd;
-      const int groups = 5;
-      for (int g = 0; g < groups; g++) {
-        const int* tbl = g == 0 ? e.items() : g == 1 ? e.pods() : g == 2 ? e.drops() : g == 3 ? e.dests() : e.dirtpos();
-        const int n = e.H(g == 0 ? H_N_ITEMS : g == 1 ? H_N_PODS : g == 2 ? H_N_DROPS : g == 3 ? H_N_DESTS : H_N_DIRT);
-        const int base = g == 0 ? e.H(H_ITEM_BASE) : g == 1 ? e.H(H_POD_BASE) : g == 2 ? e.H(H_DROP_BASE)
-                       : g == 3 ? e.H(H_DEST_BASE) : 0;
-        for (int i = 0; i < n; i++) {
-          const int w = uni(tbl[i]);
-          if (!(w & EW_PRESENT)) continue;
-          const int cell = EW_POS(w);
-          if (!near(cell)) continue;
-          const int id = g == 4 ? uni(e.dirtid()[i]) : base + i;
-          const int rE = first_visit<MAXPTS>(rv, cell);
-          if (rE >= (1 << 30)) continue;
-          // partners: wall, door, and entities of later groups with the same id
-          bool lose = false;
-          if (id < nw) {
-            const int wc = S->wall_cells[id];
-            if (near(wc)) {
-              const int rW = first_visit<MAXPTS>(rv, wc);
-              if (rW < rE) lose = true;
-              else if (rW < (1 << 30) && n_sup_walls < 8) sup_walls[n_sup_walls++] = wc;
-            }
-          }
-          if (id < ndr && (e.door()[id] & DW_PRESENT)) {
-            const int dc = S->door_cells[id];
-            if (near(dc)) {
-              const int rD = first_visit<MAXPTS>(rv, dc);
-              if (rD < rE) lose = true;
-              else if (rD < (1 << 30)) sup_doors |= 1ull << id;
-            }
-          }
-          for (int g2 = g + 1; g2 < groups; g2++) {
-            const int* t2 = g2 == 1 ? e.pods() : g2 == 2 ? e.drops() : g2 == 3 ? e.dests() : e.dirtpos();
-            const int n2 = e.H(g2 == 1 ? H_N_PODS : g2 == 2 ? H_N_DROPS : g2 == 3 ? H_N_DESTS : H_N_DIRT);
-            const int b2 = g2 == 1 ? e.H(H_POD_BASE) : g2 == 2 ? e.H(H_DROP_BASE) : g2 == 3 ? e.H(H_DEST_BASE) : 0;
-            for (int j = 0; j < n2; j++) {
-              const int w2 = uni(t2[j]);
-              if (!(w2 & EW_PRESENT)) continue;
-              const int id2 = g2 == 4 ? uni(e.dirtid()[j]) : b2 + j;
-              if (id2 != id) continue;
-              const int c2 = EW_POS(w2);
-              if (!near(c2)) continue;
-              const int r2 = first_visit<MAXPTS>(rv, c2);
-              if (r2 >= (1 << 30)) continue;
-              u64 bit = 1ull << j;
-              if (r2 < rE) lose = true;
-              else if (g2 == 1) sup_pods |= bit;
-              else if (g2 == 2) sup_drops |= bit;
-              else if (g2 == 3) sup_dests |= bit;
-              else sup_dirt |= bit;
-            }
-          }
-          if (lose) {
-            const u64 bit = 1ull << i;
-            if (g == 0) sup_items |= bit;
-            else if (g == 1) sup_pods |= bit;
-            else if (g == 2) sup_drops |= bit;
-            else if (g == 3) sup_dests |= bit;
-            else sup_dirt |= bit;
-          }
+      const int reach = d;
+      for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
+        const int q = q0 + lane;
+        bool nearq = false;
+        int cA = 0, cB = 0;
+        if (q < npairs) {
+          cA = pairs[4 * q]; cB = pairs[4 * q + 1];
+          nearq = abs(cA / W - ox) <= reach && abs(cA % W - oy) <= reach && abs(cB / W - ox) <= reach &&
+                  abs(cB % W - oy) <= reach;
         }
-      }
-      // static Wall[k] / Door[k] pairs
-      const int kmax = nw < ndr ? nw : ndr;
-      for (int k = 0; k < kmax; k++) {
-        if (!(e.door()[k] & DW_PRESENT)) continue;
-        const int wc = S->wall_cells[k], dc = S->door_cells[k];
-        if (!near(wc) || !near(dc)) continue;
-        const int rW = first_visit<MAXPTS>(rv, wc), rD = first_visit<MAXPTS>(rv, dc);
-        if (rW >= (1 << 30) || rD >= (1 << 30)) continue;
-        if (rW < rD) sup_doors |= 1ull << k;
-        else if (n_sup_walls < 8) sup_walls[n_sup_walls++] = wc;
+        u64 m = ballot(nearq);
+        while (m) {
+          const int L = ffs64(m);
+          m &= m - 1;
+          const int ca = rl(cA, L), cb = rl(cB, L);
+          const int rA = first_visit<MAXPTS>(rv, ca), rB = first_visit<MAXPTS>(rv, cb);
+          if (rA >= (1 << 30) || rB >= (1 << 30)) continue;
+          const int qq = q0 + L;
+          if (rA < rB) sup_add(sup, pairs[4 * qq + 3], cb);
+          else sup_add(sup, pairs[4 * qq + 2], ca);
+        }
       }
     }
-    // ---- placement: lane = window cell ----
+    // ---- placement (lane = window cell) ----
     {
-      const bool inwin = lane < dd;
-      const int px = lane / d, py = lane % d;
-      const int x = ax - r + px, y = ay - r + py;
-      const bool ing = inwin && x >= 0 && y >= 0 && x < S->s.H && y < W;
-      const int cell = ing ? x * W + y : -1;
-      const bool v = inwin && ((vis >> lane) & 1) && ing;
-      // per-tag values at this cell
+      const int x = ax - r + wpx, y = ay - r + wpy;
+      const bool ing = inwin && x >= 0 && y >= 0 && x < H && y < W;
+      const int cell = ing ? x * W + y : 0;
+      const bool v = ing && ((vis >> lane) & 1);
       double t_wall = 0, t_door = 0, t_item = 0, t_pod = 0, t_drop = 0, t_dirt = 0, t_dest = 0;
       u64 amask = 0;
-      if (v) {
-        if (S->level[cell] == 1) {
-          bool s = false;
-          for (int q = 0; q < n_sup_walls; q++) s |= sup_walls[q] == cell;
-          if (!s) t_wall = 1.0;
-        }
-        const int dI = door_idx(e, cell);
-        if (dI >= 0) {
-          const int w = e.door()[dI];
-          if ((w & DW_PRESENT) && !((sup_doors >> dI) & 1)) t_door = (w & DW_OPEN) ? 0.4444 : 0.6666;
-        }
-        for (int b = 0; b < A; b++)
-          if (e.agpos()[b] == cell) amask |= 1ull << b;
-        int n = e.H(H_N_ITEMS);
-        for (int i = 0; i < n; i++) {
-          const int w = e.items()[i];
-          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_items >> i) & 1)) t_item += 1.0;
-        }
-        n = e.H(H_N_PODS);
-        for (int i = 0; i < n; i++) {
-          const int w = e.pods()[i];
-          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_pods >> i) & 1)) t_pod += 1.0;
-        }
-        n = e.H(H_N_DROPS);
-        for (int i = 0; i < n; i++) {
-          const int w = e.drops()[i];
-          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_drops >> i) & 1)) t_drop += 1.0;
-        }
-        n = e.H(H_N_DESTS);
-        for (int i = 0; i < n; i++) {
-          const int w = e.dests()[i];
-          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_dests >> i) & 1)) t_dest += (w & EW_REACHED) ? 0.0 : 1.0;
-        }
-        n = e.H(H_N_DIRT);
-        for (int i = 0; i < n; i++) {
-          const int w = e.dirtpos()[i];
-          if (EW_POS(w) == cell && (w & EW_PRESENT) && !((sup_dirt >> i) & 1)) t_dirt += e.dirtamt()[i];
-        }
+      const int dI = v ? door_idx(e, cell) : -1;
+      if (v && ((S->wall_bits[cell >> 5] >> (cell & 31)) & 1u) && !((sup.walls >> lane) & 1)) t_wall = 1.0;
+      if (dI >= 0) {
+        const int w = e.door()[dI];
+        if ((w & DW_PRESENT) && !((sup.doors >> dI) & 1)) t_door = (w & DW_OPEN) ? 0.4444 : 0.6666;
+      }
+      for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
+      for (int i = 0; i < nI; i++) {
+        const int w = rl(itw, i);
+        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.items >> i) & 1)) t_item += 1.0;
+      }
+      for (int i = 0; i < nP; i++) {
+        const int w = rl(pdw, i);
+        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.pods >> i) & 1)) t_pod += 1.0;
+      }
+      for (int i = 0; i < nR; i++) {
+        const int w = rl(drw, i);
+        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.drops >> i) & 1)) t_drop += 1.0;
+      }
+      for (int i = 0; i < nS; i++) {
+        const int w = rl(dsw, i);
+        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dests >> i) & 1)) t_dest += (w & EW_REACHED) ? 0.0 : 1.0;
+      }
+      for (int i = 0; i < nT; i++) {
+        const int w = rl(dtw, i);
+        const double am = rld(dta, i);
+        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) t_dirt += am;
       }
       auto tagv = [&](int tag) -> double {
         switch (tag) {
@@ -1157,12 +1288,11 @@ __device__ void build_obs(const Env& e, OT* out_env) {
           if (lane == 0) val = frozen ? e.fbat()[a] : e.bat()[a];
         } else if (ly.kind == MFG_LAYER_GLOBALPOS) {
           const int gp = frozen ? e.fgp()[a] : apos;
-          if (lane == 0) val = (double)(gp / W) / (double)S->s.H;
+          if (lane == 0) val = (double)(gp / W) / (double)H;
           if (lane == 1) val = (double)(gp % W) / (double)W;
         }
         if (inwin) out_a[(size_t)l * dd + lane] = (OT)val;
       }
-      // padding layers (agents with fewer layers than lmax) stay untouched: zeroed once by the host
     }
   }
   e.setH(H_OBS_INIT, 1);
@@ -1195,7 +1325,8 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
     for (int r = 0; r < nr && !o.crashed; r++) rule_post_step(e, o, r);
   if (!o.crashed)
     for (int r = 0; r < nr; r++) rule_check_done(e, o, r);
-  pay_debt(e);  // eager replay of this step's membership-only shuffles
+  // the step's membership-only shuffles stay as debt: paid by k_replay after the launch, or inline by
+  // the next order-dependent consumer (spawn / reset)
   if (o.crashed || e.H(H_OVERFLOW)) {
     o.crashed = 1;
     o.done = 1;
@@ -1241,7 +1372,15 @@ __device__ __forceinline__ bool wave_env(const MfgDevSpec* S, uint8_t* smem, lon
   env = (long long)blockIdx.x * MFG_WPB + wid;
   e.S = S;
   e.lds = smem + (size_t)wid * S->lds_per_wave;
+  e.scratch = (int*)(e.lds + S->L.size);
+  e.jtab = (uint32_t*)(e.lds + S->L.size + 2048);
+  e.light = e.jtab + S->nf + 4;
+  e.hdrp = (int*)(e.lds + S->L.o_hdr);
   e.lane = lane_id();
+  if (env < B) {
+    for (int i = e.lane; i <= S->nf; i += MFG_WAVE) e.jtab[i] = 0u;
+    wave_sync();
+  }
   return env < B;
 }
 
@@ -1256,7 +1395,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S, uin
   if (!wave_env(S, smem, B, e, env)) return;
   if (mask && !mask[env]) return;
   uint8_t* rec = state + (size_t)env * S->L.size;
-  int* scratch = (int*)(e.lds + S->L.size);
+  int* scratch = e.scratch;
   if (init) {
     for (int i = e.lane; i < (S->L.size >> 2); i += MFG_WAVE) ((int*)e.lds)[i] = 0;
     wave_sync();
@@ -1286,6 +1425,48 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S, uin
   rec_store(e, rec);
 }
 
+// Pay every env's pending floor-shuffle debt. Touches only the header, MT state and floor permutation
+// of each record (the obs/step state stays in HBM), so it runs at high occupancy.
+__global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S, uint8_t* state, long long B) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int wid = threadIdx.x >> 6;
+  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  if (env >= B) return;
+  uint8_t* rec = state + (size_t)env * S->L.size;
+  const int debt = ((const int*)(rec + S->L.o_hdr))[H_DEBT];
+  if (debt == 0) return;
+  // LDS slice laid out like the record prefix so Env accessors work: [hdr .. o_mt .. o_perm end]
+  Env e;
+  e.S = S;
+  e.lds = smem + (size_t)wid * S->lds_replay_per_wave - S->L.o_mt + 4 * MFG_HDR_N;
+  e.lane = lane_id();
+  e.scratch = nullptr;
+  e.light = nullptr;
+  e.jtab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_jtab_off);
+  e.hdrp = (int*)(smem + (size_t)wid * S->lds_replay_per_wave);
+  int* hdr = e.hdr();
+  const int nmt = (S->L.o_perm + 2 * S->nf - S->L.o_mt + 15) >> 4;  // MT + perm bytes, 16 B units
+  // header: lanes copy 32 ints; MT + perm: 16 B per lane
+  if (e.lane < MFG_HDR_N) hdr[e.lane] = ((const int*)(rec + S->L.o_hdr))[e.lane];
+  {
+    const uint4* src = (const uint4*)(rec + S->L.o_mt);
+    uint4* dst = (uint4*)(e.lds + S->L.o_mt);
+    for (int i = e.lane; i < nmt; i += MFG_WAVE) dst[i] = src[i];
+  }
+  for (int i = e.lane; i <= S->nf; i += MFG_WAVE) e.jtab[i] = 0u;
+  wave_sync();
+  pay_debt(e);
+  {
+    const uint4* src = (const uint4*)(e.lds + S->L.o_mt);
+    uint4* dst = (uint4*)(rec + S->L.o_mt);
+    for (int i = e.lane; i < nmt; i += MFG_WAVE) dst[i] = src[i];
+  }
+  if (e.lane == 0) {
+    ((int*)(rec + S->L.o_hdr))[H_DEBT] = 0;
+    ((int*)(rec + S->L.o_hdr))[H_MT_IDX] = hdr[H_MT_IDX];
+  }
+}
+
 template <int MAXPTS, typename OT>
 __global__ void __launch_bounds__(MFG_WPB * 64) k_step(const MfgDevSpec* S, uint8_t* state, long long B, int K,
                                                        const int32_t* actions, unsigned philox_seed,
@@ -1297,7 +1478,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_step(const MfgDevSpec* S, uint
   long long env;
   if (!wave_env(S, smem, B, e, env)) return;
   uint8_t* rec = state + (size_t)env * S->L.size;
-  int* scratch = (int*)(e.lds + S->L.size);
+  int* scratch = e.scratch;
   const int A = S->A;
   rec_load(e, rec);
   for (int k = 0; k < K; k++) {
@@ -1316,7 +1497,9 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_step(const MfgDevSpec* S, uint
     env_step(e, my_act, o, scratch);
     write_step_outputs(e, o, row, reward, done, ev_act, ev_watch, ev_misc);
     if (o.done && auto_reset) env_reset(e, scratch);
+#ifndef MFG_ABLATE_NOOBS
     if (obs) build_obs<MAXPTS, OT>(e, obs + row * A * S->obs_agent_stride);
+#endif
   }
   rec_store(e, rec);
 }
@@ -1454,11 +1637,30 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   if (imax > 64 || pmax > 64 || dropmax > 64 || destmax > 64) { delete e; return fail("group quantity > 64"); }
   h.imax = imax; h.pmax = pmax; h.dropmax = dropmax; h.destmax = destmax;
   make_layout(s, &h.L, imax, pmax, dropmax, destmax);
-  h.lds_per_wave = align_up(h.L.size + 4 * 64, 16);
+  h.lds_per_wave = align_up(h.L.size + 2048 + 4 * (h.nf + 4) + 4 * ((HW + 31) / 32), 16);
+  // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][jtab]
+  {
+    const int mtperm = align_up(h.L.o_perm + 2 * h.nf - h.L.o_mt, 16);
+    h.replay_jtab_off = 4 * MFG_HDR_N + mtperm;
+    h.lds_replay_per_wave = align_up(h.replay_jtab_off + 4 * (h.nf + 4), 16);
+  }
   pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
   // static tables
   std::vector<uint8_t> door_of(HW, 0xFF);
   for (int d = 0; d < s->n_doors; d++) door_of[s->door_cells[d]] = (uint8_t)d;
+  std::vector<uint32_t> wall_bits((HW + 31) / 32, 0u);
+  for (int c = 0; c < HW; c++)
+    if (s->level[c] == 1) wall_bits[c >> 5] |= 1u << (c & 31);
+  std::vector<int32_t> wd;
+  const int reach = 2 * s->pomdp_r + 1;
+  for (int k = 0; k < s->n_walls && k < s->n_doors; k++) {
+    const int wc = s->wall_cells[k], dc = s->door_cells[k];
+    const int dx = wc / s->W - dc / s->W, dy = wc % s->W - dc % s->W;
+    if ((dx < 0 ? -dx : dx) <= 2 * reach && (dy < 0 ? -dy : dy) <= 2 * reach) {
+      wd.push_back(k); wd.push_back(wc); wd.push_back(dc);
+    }
+  }
+  h.n_wd_pairs = (int)(wd.size() / 3);
   std::vector<int8_t> rp((size_t)h.nrays * h.maxpts * 2, 0);
   std::vector<uint8_t> rlen(h.nrays);
   for (int r = 0; r < h.nrays; r++) {
@@ -1478,6 +1680,8 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   rc |= upload(e, s->floor_cells, s->n_floor, &h.floor_init);
   rc |= upload(e, rp.data(), rp.size(), &h.ray_pts);
   rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
+  rc |= upload(e, wall_bits.data(), wall_bits.size(), &h.wall_bits);
+  rc |= upload(e, wd.data(), wd.size(), &h.wd_pairs);
   if (rc) { delete e; return -1; }
   if (hipMalloc((void**)&e->d_spec, sizeof(MfgDevSpec)) != hipSuccess ||
       hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1564,6 +1768,18 @@ extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_
 // reward [K][B][A] f64, done [K][B] u8, obs [K][B][A][lmax][d][d], ev_act/ev_watch [K][B][A] u8,
 // ev_misc [K][B][10] i32. auto_reset: envs that finish are reset in-kernel (the obs row is then the
 // first observation of the new episode).
+// Pay all pending floor-shuffle debt (membership-only shuffles of the reference's move checks, Q3).
+extern "C" int mfg_replay(mfg_engine* e, void* stream) {
+  if (!e) return fail("null engine");
+  const unsigned grid = (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB);
+  const size_t lds = (size_t)e->h.lds_replay_per_wave * MFG_WPB;
+  hipLaunchKernelGGL(k_replay, dim3(grid), dim3(MFG_WPB * 64), lds, (hipStream_t)stream, e->d_spec, e->d_state,
+                     (long long)e->B);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
+  return 0;
+}
+
 extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
                         int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype,
                         uint8_t* ev_act, uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
@@ -1581,7 +1797,7 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
                                                            st)));
   }
   if (err != hipSuccess) return fail(std::string("k_step launch: ") + hipGetErrorString(err));
-  return 0;
+  return mfg_replay(e, stream);
 }
 
 // snapshots (checkpoints == fixtures): whole state buffer device<->device, B * layout.size bytes

@@ -12,7 +12,7 @@ import numpy as np
 
 from . import abi
 
-LIB_PATH = Path(__file__).resolve().parent / '_lib' / 'libmfg_hip.so'
+LIB_PATH = Path(os.environ.get('MFG_HIP_LIB') or Path(__file__).resolve().parent / '_lib' / 'libmfg_hip.so')
 EV_MISC = 10
 
 LAYOUT_KEYS = ['size', 'o_hdr', 'o_rule_ctr', 'o_agent_pos', 'o_agent_arr', 'o_agent_par', 'o_frozen_org',
@@ -49,6 +49,8 @@ def load_lib():
                            C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                            C.c_void_p]
     L.mfg_step.restype = C.c_int
+    L.mfg_replay.argtypes = [C.c_void_p, C.c_void_p]
+    L.mfg_replay.restype = C.c_int
     L.mfg_export_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.mfg_export_state.restype = C.c_int
     L.mfg_import_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]

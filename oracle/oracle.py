@@ -30,7 +30,7 @@ def build(force=False):
     if force or not LIB.exists() or LIB.stat().st_mtime < max(src.stat().st_mtime,
                                                               (HERE.parent / 'include' / 'mfg.h').stat().st_mtime):
         LIB.parent.mkdir(exist_ok=True)
-        subprocess.check_call(['gcc', '-O2', '-shared', '-fPIC', '-o', str(LIB), str(src), '-lm'])
+        subprocess.check_call(['gcc', '-O2', '-ffp-contract=off', '-shared', '-fPIC', '-o', str(LIB), str(src), '-lm'])
     return LIB
 
 
