@@ -42,6 +42,11 @@ static_assert(H__END <= MFG_HDR_N, "header overflow");
 
 #define MFG_DIRT_MAX 64
 
+// shuffle-block tables in LDS: [hash 512][rank 64][counter][pad]
+#define MFG_STAB_HASH 512
+#define MFG_STAB_CTR (MFG_STAB_HASH + 64)
+#define MFG_STAB_N (MFG_STAB_HASH + 68)
+
 // packed entity words (int32): pos in bits 0..15 (0xFFFF = VALUE_NO_POS), flags above
 #define EW_POS(w) ((w) & 0xFFFF)
 #define EW_ALIVE 0x10000     // member of its collection (Collection._data)
@@ -78,5 +83,5 @@ struct MfgDevSpec {
   uint64_t pcg_init_hi, pcg_init_lo, pcg_inc_hi, pcg_inc_lo;  // default_rng(env_seed) state after seeding
   MfgLayout L;
   int32_t lds_per_wave;      // bytes of dynamic LDS per wave (k_step / k_reset)
-  int32_t lds_replay_per_wave, replay_jtab_off;  // k_replay slice: [hdr][MT + perm][jtab]
+  int32_t lds_replay_per_wave, replay_jtab_off;  // k_replay slice: [hdr][MT + perm][shuffle tables]
 };

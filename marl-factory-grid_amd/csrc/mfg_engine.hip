@@ -50,11 +50,15 @@ __device__ __forceinline__ u64 wave_or64(u64 v) {
 // ------------------------------------------------------------------------------------------------
 // per-wave env context: the env record is mirrored 1:1 in the wave's LDS slice
 // ------------------------------------------------------------------------------------------------
+// The spec is read through the constant address space: uniform loads from it become scalar loads.
+#define CS __attribute__((address_space(4)))
+typedef const CS MfgDevSpec* SpecP;
+
 struct Env {
-  const MfgDevSpec* S;
+  SpecP S;
   uint8_t* lds;     // this wave's LDS slice == image of the HBM record
   int* scratch;     // 512 ints after the record (spawn positions, id-collision pairs)
-  uint32_t* jtab;   // [nf + 1] tagged max-table for the parallel shuffle blocks (not persisted)
+  uint32_t* stab;   // [MFG_STAB_N] tagged max-tables of the parallel shuffle blocks (not persisted)
   uint32_t* light;  // [(HW+31)/32] light-blocking bitmap for the ray walk (rebuilt per render)
   int* hdrp;        // header slots (inside the record image, or a separate slice in k_replay)
   int lane;
@@ -169,12 +173,15 @@ __device__ void mt_twist(const Env& e) {
 // found by Jacobi iteration with ballots (lane 0 is exact after 1 round, lane l after l+1; typical 2-3).
 //
 // If perm != null the accepted draws' Fisher-Yates swaps (i_t, j_t), t = accepted-lane order, are
-// applied as ONE parallel block instead of a serial chain. With i_t consecutive and j_t <= i_t:
+// applied as ONE parallel block instead of a serial chain. Accepted ranks t have i_t = icur - t and
+// j_t <= i_t, so:
 //   V_t (value leaving i_t) = V_{pi(t)} if pi(t) = last s<t with j_s == i_t exists, else P0[i_t]
 //   F_t (value landing on i_t) = V_{pj(t)} if pj(t) = last s<t with j_s == j_t exists, else P0[j_t]
-// (P0 = block-start values). pi comes from a tagged LDS max-table keyed by position (only s<t can have
-// j_s == i_t); pj from a loop over the few lanes that have a later equal j; V by pointer jumping.
+// (P0 = block-start values). pi comes from a 64-entry tagged max-table keyed by rank (icur - j_s);
+// pj from a loop over the lanes that may have a later equal j (found with a 512-entry hashed max-table,
+// candidates verified exactly with readlane); V by pointer jumping.
 // Writes: perm[i_t] = F_t; perm[j_t] = V_t unless a later lane rewrites j_t or j_t is a later i.
+// Tables are tagged with a per-wave chunk counter (stab[MFG_STAB_CTR]) so they are never cleared.
 // Returns j of the first accepted draw (i == hi), used by empty_positions().pop().
 __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
   uint32_t* mt = e.mt();
@@ -182,6 +189,9 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
   int idx = e.H(H_MT_IDX);
   int icur = hi;
   int first_j = -1;
+  uint32_t* htab = e.stab;                  // [MFG_STAB_HASH] j-hash -> tag | max lane
+  uint32_t* ptab = e.stab + MFG_STAB_HASH;  // [64] rank -> tag | max lane with j == i_rank
+  uint32_t ctr = perm ? (uint32_t)uni((int)e.stab[MFG_STAB_CTR]) : 0u;
   while (icur >= lo) {
     if (idx >= 624) {
       mt_twist(e);
@@ -189,7 +199,7 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
     }
     const int lmax = 624 - idx;
     const bool has = lane < lmax;
-    const uint32_t y = has ? mt_temper(mt[idx + lane]) : 0u;
+    const uint32_t y = mt_temper(mt[has ? idx + lane : 623]);
     int A = lane;
     u64 accm;
     int il;
@@ -212,28 +222,32 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
     if (first_j < 0 && nacc) first_j = rl((int)r, ffs64(accm));
 #ifndef MFG_ABLATE_NOSWAP
     if (perm && nacc) {
-      const int i = acc ? il : 0, j = acc ? (int)r : 0;
-      const int P0i = acc ? (int)perm[i] : 0;
-      const int P0j = acc ? (int)perm[j] : 0;
-      uint32_t* jtab = e.jtab;
-      const uint32_t ctr = jtab[e.S->nf] + 1u;  // tag: 26-bit chunk counter (table zeroed per launch)
+      const int i = acc ? il : icur, j = acc ? (int)r : icur;
+      const int P0i = perm[i];
+      const int P0j = perm[j];
+      ctr = (ctr + 1u) & 0x3FFFFFFu;
+      if (ctr == 0u) ctr = 1u;  // never reuse the zero tag of a freshly cleared table
       const uint32_t tag = ctr << 6;
-      if (acc) atomicMax(&jtab[j], tag | (uint32_t)lane);
+      const int imin = icur - nacc + 1;
+      const int hj = j & (MFG_STAB_HASH - 1);
+      if (acc) atomicMax(&htab[hj], tag | (uint32_t)lane);
+      if (acc && j >= imin) atomicMax(&ptab[icur - j], tag | (uint32_t)lane);
       wave_sync();
-      if (lane == 0) jtab[e.S->nf] = ctr;
-      const uint32_t tj = acc ? jtab[j] : 0u, ti = acc ? jtab[i] : 0u;
-      const bool later = acc && (tj >> 6) == ctr && (int)(tj & 63u) != lane;
+      const uint32_t th = htab[hj], tp = ptab[A & 63];
+      const bool cand = acc && (int)(th & 63u) != lane;  // some later lane shares j's hash
       int pj = -1;
-      u64 nm = ballot(later);  // lanes with a later equal j: the only possible pj targets
+      u64 later = 0;
+      u64 nm = ballot(cand);
       while (nm) {
         const int s2 = ffs64(nm);
         nm &= nm - 1;
-        const int js = rl(j, s2);
-        if (acc && s2 < lane && js == j) pj = s2;
+        const bool eq = acc && rl(j, s2) == j;
+        if (eq && s2 < lane) pj = s2;
+        if (ballot(eq && lane > s2)) later |= 1ull << s2;
       }
-      // j_s == i_t only for s <= t (j_s <= i_s < i_t for s > t); s == t is the self-swap j_t == i_t,
-      // whose predecessor on position i_t is then pj(t)
-      int pi = (acc && (ti >> 6) == ctr) ? (int)(ti & 63u) : -1;
+      // j_s == i_t only for s <= t; s == t is the self-swap j_t == i_t, whose predecessor on position
+      // i_t is then pj(t)
+      int pi = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
       if (pi == lane) pi = pj;
       int v = P0i, ptr = pi;
       while (ballot(ptr >= 0)) {
@@ -243,15 +257,15 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
       }
       const int Vj = __shfl(v, pj >= 0 ? pj : lane);
       const int F = pj >= 0 ? Vj : P0j;
-      const int imin = rl(il, 63 - __clzll((long long)accm));
       if (acc) perm[i] = (uint16_t)F;
-      if (acc && !later && !(j >= imin && j < i)) perm[j] = (uint16_t)v;
+      if (acc && !((later >> lane) & 1) && !(j >= imin && j < i)) perm[j] = (uint16_t)v;
       wave_sync();
     }
 #endif
     icur -= nacc;
     idx += consumed;
   }
+  if (perm && lane == 0) e.stab[MFG_STAB_CTR] = ctr;
   e.setH(H_MT_IDX, idx);
   wave_sync();
   return first_j;
@@ -516,7 +530,7 @@ __device__ double dirt_global_amount(const Env& e) {  // clean_up/groups.py:27-3
 
 // DirtPiles.trigger_spawn (clean_up/groups.py:70-95); returns spawn_counter, *valid = result validity
 __device__ int dirt_trigger_spawn(const Env& e, int q, double amount, int* valid, int* scratch) {
-  const mfg_spec& s = e.S->s;
+  const CS mfg_spec& s = e.S->s;
   double u = pcg_uniform(e, -s.dirt_n_var, s.dirt_n_var);
   int n_new = (int)fabs((double)q + u);
   pay_debt(e);
@@ -597,7 +611,7 @@ __device__ __forceinline__ void add_agent_reward(const Env& e, StepOut& o, int a
   if (e.lane == a) o.my_rew += r;
 }
 
-__device__ const mfg_action& action_of(const Env& e, int a, int slot) { return e.S->s.actions[a][slot]; }
+__device__ const CS mfg_action& action_of(const Env& e, int a, int slot) { return e.S->s.actions[a][slot]; }
 
 __device__ __forceinline__ void set_agent_pos(const Env& e, int a, int cell) {
   wave_sync();
@@ -614,8 +628,8 @@ __device__ __forceinline__ void set_agent_pos(const Env& e, int a, int cell) {
 // actions (environment/actions.py, modules/*/actions.py)
 // ------------------------------------------------------------------------------------------------
 __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
-  const MfgDevSpec* S = e.S;
-  const mfg_action& ac = action_of(e, a, slot);
+  SpecP S = e.S;
+  const CS mfg_action& ac = action_of(e, a, slot);
   const int op = ac.op;
   const int pos = uni(e.agpos()[a]);
   const int W = S->s.W;
@@ -726,8 +740,8 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
 // rules (environment/rules.py, modules/*/rules.py); hook order states.py:170-226
 // ------------------------------------------------------------------------------------------------
 __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
-  const MfgDevSpec* S = e.S;
-  const mfg_rule& ru = S->s.rules[ri];
+  SpecP S = e.S;
+  const CS mfg_rule& ru = S->s.rules[ri];
   const int op = ru.op;
   if (op == MFG_RULE_DOOR_AUTOCLOSE) {  // doors/rules.py:20-28, doors/entitites.py:107-122
     if (S->nd > 0) {
@@ -811,8 +825,8 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
 }
 
 __device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
-  const MfgDevSpec* S = e.S;
-  const mfg_rule& ru = S->s.rules[ri];
+  SpecP S = e.S;
+  const CS mfg_rule& ru = S->s.rules[ri];
   const int op = ru.op;
   if (op == MFG_RULE_RESPAWN_ITEMS) {  // items/rules.py:35-43
     int c = uni(e.rctr()[ri]);
@@ -859,8 +873,8 @@ __device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
 }
 
 __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
-  const MfgDevSpec* S = e.S;
-  const mfg_rule& ru = S->s.rules[ri];
+  SpecP S = e.S;
+  const CS mfg_rule& ru = S->s.rules[ri];
   const int op = ru.op;
   if (op == MFG_RULE_DONE_MAXSTEPS) {
     if (ru.i[0] <= e.H(H_STEP)) { o.done = 1; o.done_mask |= 1 << ri; }
@@ -894,7 +908,7 @@ __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
 // reset (factory.py:134-148; global_entities.py:196-203; rules.py:182-199; SpawnEntity rules)
 // ------------------------------------------------------------------------------------------------
 __device__ void env_reset(const Env& e, int* scratch) {
-  const MfgDevSpec* S = e.S;
+  SpecP S = e.S;
   const int A = S->A;
   pay_debt(e);
   // OBSBuilder keeps the episode-1 agent / battery objects for its ray origins and bound layers
@@ -943,7 +957,7 @@ __device__ void env_reset(const Env& e, int* scratch) {
   e.setH(H_ARRIVAL, A);
   // rules' on_reset in order (states.py:45-50)
   for (int r = 0; r < S->s.n_rules; r++) {
-    const mfg_rule& ru = S->s.rules[r];
+    const CS mfg_rule& ru = S->s.rules[r];
     const int op = ru.op;
     if (op == MFG_RULE_SPAWN_BATTERIES) {
       e.setH(H_BAT_BASE, e.H(H_CNT_BATTERY));
@@ -985,14 +999,14 @@ __device__ void env_reset(const Env& e, int* scratch) {
 // observation (observation_builder.py:138-235, ray_caster.py:66-104)
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
-  const MfgDevSpec* S = e.S;
+  SpecP S = e.S;
   if (x < 0 || y < 0 || x >= S->s.H || y >= S->s.W) return false;
   const int c = x * S->s.W + y;
   return (e.light[c >> 5] >> (c & 31)) & 1u;
 }
 // per-env light-blocking bitmap: walls (static) | closed doors present in the global pos_dict
 __device__ void build_light(const Env& e) {
-  const MfgDevSpec* S = e.S;
+  SpecP S = e.S;
   const int nw = (S->HW + 31) >> 5;
   for (int w = e.lane; w < nw; w += MFG_WAVE) e.light[w] = S->wall_bits[w];
   wave_sync();
@@ -1006,18 +1020,30 @@ __device__ void build_light(const Env& e) {
   wave_sync();
 }
 
-template <int MAXPTS>
-struct RayVis {
-  int cell[MAXPTS];  // visible cells of this lane's ray (-1 if none/not visible)
+// One ray per lane: packed (dx, dy) int8 offsets of up to 16 points and the ray length.
+struct RayLane {
+  uint32_t pk[4];  // byte 2p = dx of point p, byte 2p+1 = dy (sign-extended on use)
+  int len;
+  __device__ __forceinline__ int dx(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16)) & 0xFF); }
+  __device__ __forceinline__ int dy(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16 + 8)) & 0xFF); }
 };
 
-// rank of the first visit of `cell` (ray index * 32 + point index), or a large value if not visible
+// Visible points of this lane's ray for one origin: bit p set = point p added entities (not diagonal-cut,
+// in the grid, before the walk stopped).
+struct RayVis {
+  uint32_t vism;
+  int ox, oy, W;
+  const RayLane* rl_;
+};
+
+// rank of the first visit of `cell` (ray index * 32 + point index), or 1<<30 if not visible
 template <int MAXPTS>
-__device__ int first_visit(const RayVis<MAXPTS>& rv, int cell) {
+__device__ int first_visit(const RayVis& rv, int cell) {
   int k = -1;
+  const int cx = cell / rv.W, cy = cell % rv.W;
 #pragma unroll
   for (int p = 0; p < MAXPTS; p++)
-    if (k < 0 && rv.cell[p] == cell) k = p;
+    if (k < 0 && ((rv.vism >> p) & 1u) && rv.ox + rv.rl_->dx(p) == cx && rv.oy + rv.rl_->dy(p) == cy) k = p;
   const u64 m = ballot(k >= 0);
   if (!m) return 1 << 30;
   const int L = ffs64(m);
@@ -1029,7 +1055,7 @@ __device__ int first_visit(const RayVis<MAXPTS>& rv, int cell) {
 // 6 dirt, 7 dest, 9 wall -> slot unused, the wall is identified by its cell). Returns the pair count.
 #define OBS_MAX_PAIRS 120
 __device__ int build_id_pairs(const Env& e, int* pairs) {
-  const MfgDevSpec* S = e.S;
+  SpecP S = e.S;
   const int lane = e.lane;
   // concatenated dynamic int-id entities: items, pods, drops, dests, dirt (<= 64 in total for dedupe)
   const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
@@ -1128,7 +1154,7 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int cell) {
 
 template <int MAXPTS, typename OT>
 __device__ void build_obs(const Env& e, OT* out_env) {
-  const MfgDevSpec* S = e.S;
+  SpecP S = e.S;
   const int A = S->A, H = S->s.H, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
   const int lane = e.lane;
   const bool frozen = e.H(H_FROZEN) != 0;
@@ -1145,16 +1171,21 @@ __device__ void build_obs(const Env& e, OT* out_env) {
   const int dsw = lane < nS ? e.dests()[lane] : 0;
   const int dtw = lane < nT ? e.dirtpos()[lane] : 0;
   const double dta = lane < nT ? e.dirtamt()[lane] : 0.0;
-  // this lane's ray: (dx, dy) of every point, loaded once
-  const bool has_ray = lane < S->nrays;
-  const int rlen = has_ray ? S->ray_len[lane] : 0;
-  int rdx[MAXPTS], rdy[MAXPTS];
+  // this lane's ray, loaded once: 16 packed bytes
+  RayLane ray;
   {
-    const int8_t* pts = S->ray_pts + (size_t)(has_ray ? lane : 0) * MAXPTS * 2;
+    const bool has = lane < S->nrays;
+    const int8_t* pts = S->ray_pts + (size_t)(has ? lane : 0) * MAXPTS * 2;
 #pragma unroll
-    for (int p = 0; p < MAXPTS; p++) { rdx[p] = pts[2 * p]; rdy[p] = pts[2 * p + 1]; }
+    for (int q = 0; q < 4; q++) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (4 * q + b < 2 * MAXPTS) w |= (uint32_t)(uint8_t)pts[4 * q + b] << (8 * b);
+      ray.pk[q] = w;
+    }
+    ray.len = has ? S->ray_len[lane] : 0;
   }
-  // this lane's window cell
   const bool inwin = lane < dd;
   const int wpx = lane / d, wpy = lane % d;
   for (int a = 0; a < A; a++) {
@@ -1162,137 +1193,124 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     const int ax = apos / W, ay = apos % W;
     const int org = rl(org_l, a);
     const int ox = org / W, oy = org % W;
-    // ---- ray walk (lane = ray): all blocking lookups issued up front, then the walk in registers ----
-    RayVis<MAXPTS> rv;
+    // ---- ray walk (lane = ray): blocking bits of all points first, then the walk on bitmasks ----
+    uint32_t blkm = 0, cutm = 0, ing = 0;
+#pragma unroll
+    for (int p = 0; p < MAXPTS; p++) {
+      const int x = ox + ray.dx(p), y = oy + ray.dy(p);
+      ing |= (x >= 0 && y >= 0 && x < H && y < W) ? (1u << p) : 0u;
+      blkm |= light_block(e, x, y) ? (1u << p) : 0u;
+      if (p > 0 && ray.dx(p) != ray.dx(p - 1) && ray.dy(p) != ray.dy(p - 1)) {
+        // diagonal step: cut when both orthogonal neighbours block light (ray_caster.py:89-96)
+        const bool c = light_block(e, x, oy + ray.dy(p - 1)) && light_block(e, ox + ray.dx(p - 1), y);
+        cutm |= c ? (1u << p) : 0u;
+      }
+    }
+    // points walked: up to and including the first blocking/cut point, within the ray length
+    const uint32_t lenm = ray.len >= 32 ? 0xFFFFFFFFu : ((1u << ray.len) - 1u);
+    const uint32_t stopm = (blkm | cutm) & lenm;
+    const uint32_t walked = stopm ? (((stopm & (0u - stopm)) << 1) - 1u) & lenm : lenm;
+    RayVis rv;
+    rv.vism = walked & ~cutm & ing;
+    rv.ox = ox; rv.oy = oy; rv.W = W; rv.rl_ = &ray;
     u64 wmask = 0;
-    {
-      bool blk[MAXPTS], cut[MAXPTS];
-      int cx_[MAXPTS], cy_[MAXPTS];
 #pragma unroll
-      for (int p = 0; p < MAXPTS; p++) {
-        const int x = ox + rdx[p], y = oy + rdy[p];
-        cx_[p] = x; cy_[p] = y;
-        blk[p] = light_block(e, x, y);
-        if (p > 0 && rdx[p] != rdx[p - 1] && rdy[p] != rdy[p - 1]) {
-          // diagonal step: cut when both orthogonal neighbours block light (ray_caster.py:89-96)
-          cut[p] = light_block(e, x, oy + rdy[p - 1]) && light_block(e, ox + rdx[p - 1], y);
-        } else {
-          cut[p] = false;
-        }
-      }
-      bool alive = has_ray;
-#pragma unroll
-      for (int p = 0; p < MAXPTS; p++) {
-        rv.cell[p] = -1;
-        if (alive && p < rlen) {
-          const int x = cx_[p], y = cy_[p];
-          if (!cut[p] && x >= 0 && y >= 0 && x < H && y < W) {
-            rv.cell[p] = x * W + y;
-            const int px = x - ax + r, py = y - ay + r;
-            if (px >= 0 && py >= 0 && px < d && py < d) wmask |= 1ull << (px * d + py);
-          }
-          if (blk[p] || cut[p]) alive = false;
-        }
-      }
+    for (int p = 0; p < MAXPTS; p++) {
+      const int px = ox + ray.dx(p) - ax + r, py = oy + ray.dy(p) - ay + r;
+      if (((rv.vism >> p) & 1u) && px >= 0 && py >= 0 && px < d && py < d) wmask |= 1ull << (px * d + py);
     }
     const u64 vis = wave_or64(wmask);
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     Sup sup;
     sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = sup.walls = 0;
     sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
-    {
-      const int reach = d;
-      for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
-        const int q = q0 + lane;
-        bool nearq = false;
-        int cA = 0, cB = 0;
-        if (q < npairs) {
-          cA = pairs[4 * q]; cB = pairs[4 * q + 1];
-          nearq = abs(cA / W - ox) <= reach && abs(cA % W - oy) <= reach && abs(cB / W - ox) <= reach &&
-                  abs(cB % W - oy) <= reach;
-        }
-        u64 m = ballot(nearq);
-        while (m) {
-          const int L = ffs64(m);
-          m &= m - 1;
-          const int ca = rl(cA, L), cb = rl(cB, L);
-          const int rA = first_visit<MAXPTS>(rv, ca), rB = first_visit<MAXPTS>(rv, cb);
-          if (rA >= (1 << 30) || rB >= (1 << 30)) continue;
-          const int qq = q0 + L;
-          if (rA < rB) sup_add(sup, pairs[4 * qq + 3], cb);
-          else sup_add(sup, pairs[4 * qq + 2], ca);
-        }
+    for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
+      const int q = q0 + lane;
+      const int cA = q < npairs ? pairs[4 * q] : 0, cB = q < npairs ? pairs[4 * q + 1] : 0;
+      const bool nearq = q < npairs && abs(cA / W - ox) <= d && abs(cA % W - oy) <= d && abs(cB / W - ox) <= d &&
+                         abs(cB % W - oy) <= d;
+      u64 m = ballot(nearq);
+      while (m) {
+        const int L = ffs64(m);
+        m &= m - 1;
+        const int ca = rl(cA, L), cb = rl(cB, L);
+        const int rA = first_visit<MAXPTS>(rv, ca), rB = first_visit<MAXPTS>(rv, cb);
+        if (rA >= (1 << 30) || rB >= (1 << 30)) continue;
+        const int qq = q0 + L;
+        if (rA < rB) sup_add(sup, pairs[4 * qq + 3], cb);
+        else sup_add(sup, pairs[4 * qq + 2], ca);
       }
     }
-    // ---- placement (lane = window cell) ----
+    // ---- placement (lane = window cell): presence bits per tag, values composed per layer ----
+    const int x = ax - r + wpx, y = ay - r + wpy;
+    const bool v = inwin && x >= 0 && y >= 0 && x < H && y < W && ((vis >> lane) & 1);
+    const int cell = v ? x * W + y : 0;
+    uint32_t tags = 0;  // bit t = tag t (< 16) has an entity here
+    float door_enc = 0.f;
+    double dirt_amt = 0.0;
+    if (v && ((S->wall_bits[cell >> 5] >> (cell & 31)) & 1u) && !((sup.walls >> lane) & 1)) tags |= 1u << MFG_TAG_WALLS;
     {
-      const int x = ax - r + wpx, y = ay - r + wpy;
-      const bool ing = inwin && x >= 0 && y >= 0 && x < H && y < W;
-      const int cell = ing ? x * W + y : 0;
-      const bool v = ing && ((vis >> lane) & 1);
-      double t_wall = 0, t_door = 0, t_item = 0, t_pod = 0, t_drop = 0, t_dirt = 0, t_dest = 0;
-      u64 amask = 0;
       const int dI = v ? door_idx(e, cell) : -1;
-      if (v && ((S->wall_bits[cell >> 5] >> (cell & 31)) & 1u) && !((sup.walls >> lane) & 1)) t_wall = 1.0;
       if (dI >= 0) {
         const int w = e.door()[dI];
-        if ((w & DW_PRESENT) && !((sup.doors >> dI) & 1)) t_door = (w & DW_OPEN) ? 0.4444 : 0.6666;
+        if ((w & DW_PRESENT) && !((sup.doors >> dI) & 1)) tags |= 1u << MFG_TAG_DOORS;
+        door_enc = (w & DW_OPEN) ? 1.f : 0.f;
       }
-      for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
-      for (int i = 0; i < nI; i++) {
-        const int w = rl(itw, i);
-        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.items >> i) & 1)) t_item += 1.0;
-      }
-      for (int i = 0; i < nP; i++) {
-        const int w = rl(pdw, i);
-        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.pods >> i) & 1)) t_pod += 1.0;
-      }
-      for (int i = 0; i < nR; i++) {
-        const int w = rl(drw, i);
-        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.drops >> i) & 1)) t_drop += 1.0;
-      }
-      for (int i = 0; i < nS; i++) {
-        const int w = rl(dsw, i);
-        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dests >> i) & 1)) t_dest += (w & EW_REACHED) ? 0.0 : 1.0;
-      }
-      for (int i = 0; i < nT; i++) {
-        const int w = rl(dtw, i);
-        const double am = rld(dta, i);
-        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) t_dirt += am;
-      }
-      auto tagv = [&](int tag) -> double {
-        switch (tag) {
-          case MFG_TAG_WALLS: return t_wall;
-          case MFG_TAG_DOORS: return t_door;
-          case MFG_TAG_ITEMS: return t_item;
-          case MFG_TAG_PODS: return t_pod;
-          case MFG_TAG_DROPOFFS: return t_drop;
-          case MFG_TAG_DIRT: return t_dirt;
-          case MFG_TAG_DESTS: return t_dest;
-          default:
-            if (tag >= MFG_TAG_AGENT0) return ((amask >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
-            return 0.0;
+    }
+    u64 amask = 0;
+    for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
+    for (int i = 0; i < nI; i++) {
+      const int w = rl(itw, i);
+      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.items >> i) & 1)) tags |= 1u << MFG_TAG_ITEMS;
+    }
+    for (int i = 0; i < nP; i++) {
+      const int w = rl(pdw, i);
+      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.pods >> i) & 1)) tags |= 1u << MFG_TAG_PODS;
+    }
+    for (int i = 0; i < nR; i++) {
+      const int w = rl(drw, i);
+      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.drops >> i) & 1)) tags |= 1u << MFG_TAG_DROPOFFS;
+    }
+    for (int i = 0; i < nS; i++) {
+      const int w = rl(dsw, i);
+      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dests >> i) & 1) && !(w & EW_REACHED))
+        tags |= 1u << MFG_TAG_DESTS;
+    }
+    for (int i = 0; i < nT; i++) {
+      const int w = rl(dtw, i);
+      const double am = rld(dta, i);
+      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) { tags |= 1u << MFG_TAG_DIRT; dirt_amt = am; }
+    }
+    // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666/0.4444,
+    // dirt = amount); at most one entity per (tag, cell) in the global pos_dict
+    auto tagv = [&](int tag) -> double {
+      if (tag >= MFG_TAG_AGENT0) return ((amask >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
+      if (!((tags >> tag) & 1u)) return 0.0;
+      if (tag == MFG_TAG_DOORS) return door_enc != 0.f ? 0.4444 : 0.6666;
+      if (tag == MFG_TAG_DIRT) return dirt_amt;
+      return 1.0;
+    };
+    OT* out_a = out_env + (size_t)a * S->obs_agent_stride;
+    const int nl = S->s.n_layers[a];
+    for (int l = 0; l < nl; l++) {
+      const int kind = S->s.layers[a][l].kind;
+      double val = 0.0;
+      if (kind == MFG_LAYER_TAG) {
+        val = tagv(S->s.layers[a][l].tag);
+      } else if (kind == MFG_LAYER_COMBINED) {
+        const int nc = S->s.combined_n[a];
+        for (int q = 0; q < nc; q++) {
+          const double tv = tagv(S->s.combined_tags[a][q]);
+          val = q == 0 ? tv : val + tv;
         }
-      };
-      OT* out_a = out_env + (size_t)a * S->obs_agent_stride;
-      const int nl = S->s.n_layers[a];
-      for (int l = 0; l < nl; l++) {
-        const mfg_layer& ly = S->s.layers[a][l];
-        double val = 0.0;
-        if (ly.kind == MFG_LAYER_TAG) {
-          val = tagv(ly.tag);
-        } else if (ly.kind == MFG_LAYER_COMBINED) {
-          const int nc = S->s.combined_n[a];
-          for (int q = 0; q < nc; q++) val = q == 0 ? tagv(S->s.combined_tags[a][q]) : val + tagv(S->s.combined_tags[a][q]);
-        } else if (ly.kind == MFG_LAYER_BATTERY) {
-          if (lane == 0) val = frozen ? e.fbat()[a] : e.bat()[a];
-        } else if (ly.kind == MFG_LAYER_GLOBALPOS) {
-          const int gp = frozen ? e.fgp()[a] : apos;
-          if (lane == 0) val = (double)(gp / W) / (double)H;
-          if (lane == 1) val = (double)(gp % W) / (double)W;
-        }
-        if (inwin) out_a[(size_t)l * dd + lane] = (OT)val;
+      } else if (kind == MFG_LAYER_BATTERY) {
+        if (lane == 0) val = frozen ? e.fbat()[a] : e.bat()[a];
+      } else if (kind == MFG_LAYER_GLOBALPOS) {
+        const int gp = frozen ? e.fgp()[a] : apos;
+        if (lane == 0) val = (double)(gp / W) / (double)H;
+        if (lane == 1) val = (double)(gp % W) / (double)W;
       }
+      if (inwin) out_a[(size_t)l * dd + lane] = (OT)val;
     }
   }
   e.setH(H_OBS_INIT, 1);
@@ -1305,7 +1323,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
 #define MFG_EV_MISC 10
 
 __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
-  const MfgDevSpec* S = e.S;
+  SpecP S = e.S;
   const int A = S->A;
   o.my_rew = 0.0; o.g_rew = 0.0; o.my_act_ev = 0; o.my_watch_ev = 0; o.door_coll = 0;
   o.respawn_items_value = -1; o.dirt_spawn_value = -1; o.dirt_spawn_valid = 0; o.door_autoclose = 0;
@@ -1367,18 +1385,18 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
 // ------------------------------------------------------------------------------------------------
 #define MFG_WPB 4
 
-__device__ __forceinline__ bool wave_env(const MfgDevSpec* S, uint8_t* smem, long long B, Env& e, long long& env) {
+__device__ __forceinline__ bool wave_env(SpecP S, uint8_t* smem, long long B, Env& e, long long& env) {
   const int wid = threadIdx.x >> 6;
   env = (long long)blockIdx.x * MFG_WPB + wid;
   e.S = S;
   e.lds = smem + (size_t)wid * S->lds_per_wave;
   e.scratch = (int*)(e.lds + S->L.size);
-  e.jtab = (uint32_t*)(e.lds + S->L.size + 2048);
-  e.light = e.jtab + S->nf + 4;
+  e.stab = (uint32_t*)(e.lds + S->L.size + 2048);
+  e.light = e.stab + MFG_STAB_N;
   e.hdrp = (int*)(e.lds + S->L.o_hdr);
   e.lane = lane_id();
   if (env < B) {
-    for (int i = e.lane; i <= S->nf; i += MFG_WAVE) e.jtab[i] = 0u;
+    for (int i = e.lane; i < MFG_STAB_N; i += MFG_WAVE) e.stab[i] = 0u;
     wave_sync();
   }
   return env < B;
@@ -1386,10 +1404,11 @@ __device__ __forceinline__ bool wave_env(const MfgDevSpec* S, uint8_t* smem, lon
 
 // creation (init=1): random.seed(py_seed), Factory.__init__ (floor list, OBSBuilder shuffle); then reset
 template <int MAXPTS, typename OT>
-__global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S, uint8_t* state, long long B,
+__global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, uint8_t* state, long long B,
                                                         const uint8_t* mask, OT* obs, int init,
                                                         unsigned long long seed_base) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
   Env e;
   long long env;
   if (!wave_env(S, smem, B, e, env)) return;
@@ -1409,7 +1428,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S, uin
     }
     if (e.lane < S->nd) e.door()[e.lane] = DW_PRESENT;
     for (int r = 0; r < S->s.n_rules; r++) {
-      const mfg_rule& ru = S->s.rules[r];
+      const CS mfg_rule& ru = S->s.rules[r];
       if (e.lane == 0 && ru.op == MFG_RULE_RESPAWN_ITEMS) e.rctr()[r] = ru.i[1];
       if (e.lane == 0 && ru.op == MFG_RULE_RESPAWN_DIRT) e.rctr()[r] = ru.i[0];
     }
@@ -1427,8 +1446,9 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S, uin
 
 // Pay every env's pending floor-shuffle debt. Touches only the header, MT state and floor permutation
 // of each record (the obs/step state stays in HBM), so it runs at high occupancy.
-__global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S, uint8_t* state, long long B) {
+__global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, uint8_t* state, long long B) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
   const int wid = threadIdx.x >> 6;
   const long long env = (long long)blockIdx.x * MFG_WPB + wid;
   if (env >= B) return;
@@ -1442,7 +1462,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S, ui
   e.lane = lane_id();
   e.scratch = nullptr;
   e.light = nullptr;
-  e.jtab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_jtab_off);
+  e.stab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_jtab_off);
   e.hdrp = (int*)(smem + (size_t)wid * S->lds_replay_per_wave);
   int* hdr = e.hdr();
   const int nmt = (S->L.o_perm + 2 * S->nf - S->L.o_mt + 15) >> 4;  // MT + perm bytes, 16 B units
@@ -1453,7 +1473,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S, ui
     uint4* dst = (uint4*)(e.lds + S->L.o_mt);
     for (int i = e.lane; i < nmt; i += MFG_WAVE) dst[i] = src[i];
   }
-  for (int i = e.lane; i <= S->nf; i += MFG_WAVE) e.jtab[i] = 0u;
+  for (int i = e.lane; i < MFG_STAB_N; i += MFG_WAVE) e.stab[i] = 0u;
   wave_sync();
   pay_debt(e);
   {
@@ -1468,12 +1488,13 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S, ui
 }
 
 template <int MAXPTS, typename OT>
-__global__ void __launch_bounds__(MFG_WPB * 64) k_step(const MfgDevSpec* S, uint8_t* state, long long B, int K,
+__global__ void __launch_bounds__(MFG_WPB * 64) k_step(const MfgDevSpec* S_, uint8_t* state, long long B, int K,
                                                        const int32_t* actions, unsigned philox_seed,
                                                        unsigned env_base, long long step_base, double* reward, uint8_t* done, OT* obs,
                                                        uint8_t* ev_act, uint8_t* ev_watch, int32_t* ev_misc,
                                                        int auto_reset) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
   Env e;
   long long env;
   if (!wave_env(S, smem, B, e, env)) return;
@@ -1637,12 +1658,12 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   if (imax > 64 || pmax > 64 || dropmax > 64 || destmax > 64) { delete e; return fail("group quantity > 64"); }
   h.imax = imax; h.pmax = pmax; h.dropmax = dropmax; h.destmax = destmax;
   make_layout(s, &h.L, imax, pmax, dropmax, destmax);
-  h.lds_per_wave = align_up(h.L.size + 2048 + 4 * (h.nf + 4) + 4 * ((HW + 31) / 32), 16);
-  // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][jtab]
+  h.lds_per_wave = align_up(h.L.size + 2048 + 4 * MFG_STAB_N + 4 * ((HW + 31) / 32), 16);
+  // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     const int mtperm = align_up(h.L.o_perm + 2 * h.nf - h.L.o_mt, 16);
     h.replay_jtab_off = 4 * MFG_HDR_N + mtperm;
-    h.lds_replay_per_wave = align_up(h.replay_jtab_off + 4 * (h.nf + 4), 16);
+    h.lds_replay_per_wave = align_up(h.replay_jtab_off + 4 * MFG_STAB_N, 16);
   }
   pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
   // static tables
