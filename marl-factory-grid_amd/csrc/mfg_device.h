@@ -42,10 +42,11 @@ static_assert(H__END <= MFG_HDR_N, "header overflow");
 
 #define MFG_DIRT_MAX 64
 
-// shuffle-block tables in LDS: [hash 512][rank 64][counter][pad]
+// shuffle-block tables in LDS (u32): [rank table 64][counter][pad 3][j-hash table 512 (table path only)]
 #define MFG_STAB_HASH 512
-#define MFG_STAB_CTR (MFG_STAB_HASH + 64)
-#define MFG_STAB_N (MFG_STAB_HASH + 68)
+#define MFG_STAB_CTR 64
+#define MFG_STAB_PTAB 68
+#define MFG_STAB_N (MFG_STAB_PTAB + MFG_STAB_HASH)
 
 // packed entity words (int32): pos in bits 0..15 (0xFFFF = VALUE_NO_POS), flags above
 #define EW_POS(w) ((w) & 0xFFFF)
@@ -77,11 +78,17 @@ struct MfgDevSpec {
   const int32_t* floor_init; // [nf]
   const int8_t* ray_pts;     // [nrays][maxpts][2] (dx, dy), padded
   const uint8_t* ray_len;    // [nrays]
-  const uint32_t* wall_bits; // [(HW+31)/32] static light/position blockers (walls)
   int32_t n_wd_pairs;        // static identifier collisions Wall[k]/Door[k] that one ray fan can reach
   const int32_t* wd_pairs;   // [n_wd_pairs][3]: k, wall cell, door cell
   uint64_t pcg_init_hi, pcg_init_lo, pcg_inc_hi, pcg_inc_lo;  // default_rng(env_seed) state after seeding
+  const uint8_t* base_map;   // [map_bytes] static cell map of the obs render (CM_WALL bits)
+  int32_t map_bytes;         // HW rounded up to 16
+  int32_t step_rng;          // a rule consumes the floor order / RNG inside a step (dirt spawns)
   MfgLayout L;
-  int32_t lds_per_wave;      // bytes of dynamic LDS per wave (k_step / k_reset)
-  int32_t lds_replay_per_wave, replay_jtab_off;  // k_replay slice: [hdr][MT + perm][shuffle tables]
+  int32_t lds_full;          // bytes of dynamic LDS per wave: full record + scratch + shuffle tables
+  int32_t lds_logic;         // k_logic: lean record (o_mt bytes) or lds_full when step_rng
+  int32_t lds_obs;           // k_obs: lean record + cell map + id-collision pairs
+  int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)
+  int32_t lds_replay_per_wave;  // k_replay slice: [hdr 128 B][MT 2496 B][perm as u32][shuffle tables]
+  int32_t replay_perm_off, replay_stab_off, replay_stab_n;
 };

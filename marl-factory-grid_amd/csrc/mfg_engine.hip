@@ -59,7 +59,7 @@ struct Env {
   uint8_t* lds;     // this wave's LDS slice == image of the HBM record
   int* scratch;     // 512 ints after the record (spawn positions, id-collision pairs)
   uint32_t* stab;   // [MFG_STAB_N] tagged max-tables of the parallel shuffle blocks (not persisted)
-  uint32_t* light;  // [(HW+31)/32] light-blocking bitmap for the ray walk (rebuilt per render)
+  uint8_t* cmap;    // [HW] per-env cell map of the obs render (rebuilt per render)
   int* hdrp;        // header slots (inside the record image, or a separate slice in k_replay)
   int lane;
   __device__ int* hdr() const { return hdrp; }
@@ -91,22 +91,6 @@ struct Env {
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
-// copy record HBM <-> LDS (16 B per lane per iteration, coalesced)
-__device__ void rec_load(const Env& e, const uint8_t* g) {
-  const int n16 = e.S->L.size >> 4;
-  const uint4* src = (const uint4*)g;
-  uint4* dst = (uint4*)e.lds;
-  for (int i = e.lane; i < n16; i += MFG_WAVE) dst[i] = src[i];
-  wave_sync();
-}
-__device__ void rec_store(const Env& e, uint8_t* g) {
-  wave_sync();
-  const int n16 = e.S->L.size >> 4;
-  const uint4* src = (const uint4*)e.lds;
-  uint4* dst = (uint4*)g;
-  for (int i = e.lane; i < n16; i += MFG_WAVE) dst[i] = src[i];
-}
-
 // ------------------------------------------------------------------------------------------------
 // MT19937 (CPython semantics) — state in LDS, lane-parallel twist
 // ------------------------------------------------------------------------------------------------
@@ -132,10 +116,11 @@ __device__ void mt_twist(const Env& e) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
   uint32_t v[4];
+  // loads are unconditional (clamped indices) so each phase is one batch of LDS reads and one wait
 #pragma unroll
   for (int t = 0; t < 4; t++) {
-    const int i = t * MFG_WAVE + lane;
-    v[t] = i < 227 ? mt_mix(mt[i], mt[i + 1], mt[i + 397]) : 0u;
+    const int i = min(t * MFG_WAVE + lane, 226);
+    v[t] = mt_mix(mt[i], mt[i + 1], mt[i + 397]);
   }
 #pragma unroll
   for (int t = 0; t < 4; t++) {
@@ -144,8 +129,8 @@ __device__ void mt_twist(const Env& e) {
   }
 #pragma unroll
   for (int t = 0; t < 4; t++) {
-    const int i = 227 + t * MFG_WAVE + lane;
-    v[t] = i < 454 ? mt_mix(mt[i], mt[i + 1], mt[i - 227]) : 0u;
+    const int i = min(227 + t * MFG_WAVE + lane, 453);
+    v[t] = mt_mix(mt[i], mt[i + 1], mt[i - 227]);
   }
 #pragma unroll
   for (int t = 0; t < 4; t++) {
@@ -154,14 +139,15 @@ __device__ void mt_twist(const Env& e) {
   }
 #pragma unroll
   for (int t = 0; t < 3; t++) {
-    const int i = 454 + t * MFG_WAVE + lane;
-    v[t] = i < 623 ? mt_mix(mt[i], mt[i + 1], mt[i - 227]) : 0u;
+    const int i = min(454 + t * MFG_WAVE + lane, 622);
+    v[t] = mt_mix(mt[i], mt[i + 1], mt[i - 227]);
   }
 #pragma unroll
   for (int t = 0; t < 3; t++) {
     const int i = 454 + t * MFG_WAVE + lane;
     if (i < 623) mt[i] = v[t];
   }
+  wave_sync();
   if (lane == 0) mt[623] = mt_mix(mt[623], mt[0], mt[396]);
   wave_sync();
 }
@@ -177,20 +163,27 @@ __device__ void mt_twist(const Env& e) {
 // j_t <= i_t, so:
 //   V_t (value leaving i_t) = V_{pi(t)} if pi(t) = last s<t with j_s == i_t exists, else P0[i_t]
 //   F_t (value landing on i_t) = V_{pj(t)} if pj(t) = last s<t with j_s == j_t exists, else P0[j_t]
-// (P0 = block-start values). pi comes from a 64-entry tagged max-table keyed by rank (icur - j_s);
-// pj from a loop over the lanes that may have a later equal j (found with a 512-entry hashed max-table,
-// candidates verified exactly with readlane); V by pointer jumping.
-// Writes: perm[i_t] = F_t; perm[j_t] = V_t unless a later lane rewrites j_t or j_t is a later i.
+// (P0 = block-start values). pi comes from a 64-entry tagged max-table keyed by rank (icur - j_s,
+// self-swaps excluded); V by pointer jumping.
+//  * exchange path (32-bit perm, S->xchg_ordered): one ds_wrxchg of V_t into perm[j_t] per lane. The
+//    LDS applies a wave's conflicting lanes in ascending lane order (verified on the device by
+//    mfg_create's probe, else this path is off), so lane t gets F_t back and the last writer stays.
+//    Then perm[i_t] = F_t.
+//  * table path (16-bit perm inside the record image): pj from a loop over the lanes that may have a
+//    later equal j (512-entry hashed max-table, candidates verified exactly with readlane); writes
+//    perm[i_t] = F_t and perm[j_t] = V_t unless a later lane rewrites j_t or j_t is a later i.
 // Tables are tagged with a per-wave chunk counter (stab[MFG_STAB_CTR]) so they are never cleared.
 // Returns j of the first accepted draw (i == hi), used by empty_positions().pop().
-__device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
+template <typename PT>
+__device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
   int idx = e.H(H_MT_IDX);
   int icur = hi;
   int first_j = -1;
-  uint32_t* htab = e.stab;                  // [MFG_STAB_HASH] j-hash -> tag | max lane
-  uint32_t* ptab = e.stab + MFG_STAB_HASH;  // [64] rank -> tag | max lane with j == i_rank
+  uint32_t* ptab = e.stab;                    // [64] rank -> tag | max lane with j == i_rank
+  uint32_t* htab = e.stab + MFG_STAB_PTAB;    // [MFG_STAB_HASH] j-hash -> tag | max lane
+  const bool xchg = sizeof(PT) == 4 && e.S->xchg_ordered;
   uint32_t ctr = perm ? (uint32_t)uni((int)e.stab[MFG_STAB_CTR]) : 0u;
   while (icur >= lo) {
     if (idx >= 624) {
@@ -224,42 +217,59 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
     if (perm && nacc) {
       const int i = acc ? il : icur, j = acc ? (int)r : icur;
       const int P0i = perm[i];
-      const int P0j = perm[j];
       ctr = (ctr + 1u) & 0x3FFFFFFu;
       if (ctr == 0u) ctr = 1u;  // never reuse the zero tag of a freshly cleared table
       const uint32_t tag = ctr << 6;
       const int imin = icur - nacc + 1;
-      const int hj = j & (MFG_STAB_HASH - 1);
-      if (acc) atomicMax(&htab[hj], tag | (uint32_t)lane);
-      if (acc && j >= imin) atomicMax(&ptab[icur - j], tag | (uint32_t)lane);
-      wave_sync();
-      const uint32_t th = htab[hj], tp = ptab[A & 63];
-      const bool cand = acc && (int)(th & 63u) != lane;  // some later lane shares j's hash
-      int pj = -1;
-      u64 later = 0;
-      u64 nm = ballot(cand);
-      while (nm) {
-        const int s2 = ffs64(nm);
-        nm &= nm - 1;
-        const bool eq = acc && rl(j, s2) == j;
-        if (eq && s2 < lane) pj = s2;
-        if (ballot(eq && lane > s2)) later |= 1ull << s2;
+      if (acc && j >= imin && j != i) atomicMax(&ptab[icur - j], tag | (uint32_t)lane);
+      if (xchg) {
+        wave_sync();
+        const uint32_t tp = ptab[A & 63];
+        int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
+        int v = P0i;
+        while (ballot(ptr >= 0)) {
+          const int src = ptr >= 0 ? ptr : lane;
+          const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
+          if (ptr >= 0) { v = v2; ptr = p2; }
+        }
+        int F = 0;
+        if (acc) F = (int)atomicExch((uint32_t*)&perm[j], (uint32_t)v);
+        wave_sync();
+        if (acc) perm[i] = (PT)F;
+        wave_sync();
+      } else {
+        const int P0j = perm[j];
+        const int hj = j & (MFG_STAB_HASH - 1);
+        if (acc) atomicMax(&htab[hj], tag | (uint32_t)lane);
+        wave_sync();
+        const uint32_t th = htab[hj], tp = ptab[A & 63];
+        const bool cand = acc && (int)(th & 63u) != lane;  // some later lane shares j's hash
+        int pj = -1;
+        u64 later = 0;
+        u64 nm = ballot(cand);
+#ifdef MFG_ABLATE_NOPJ
+        nm = 0;
+#endif
+        while (nm) {
+          const int s2 = ffs64(nm);
+          nm &= nm - 1;
+          const bool eq = acc && rl(j, s2) == j;
+          if (eq && s2 < lane) pj = s2;
+          if (ballot(eq && lane > s2)) later |= 1ull << s2;
+        }
+        int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
+        int v = P0i;
+        while (ballot(ptr >= 0)) {
+          const int src = ptr >= 0 ? ptr : lane;
+          const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
+          if (ptr >= 0) { v = v2; ptr = p2; }
+        }
+        const int Vj = __shfl(v, pj >= 0 ? pj : lane);
+        const int F = pj >= 0 ? Vj : P0j;
+        if (acc) perm[i] = (PT)F;
+        if (acc && !((later >> lane) & 1) && !(j >= imin && j < i)) perm[j] = (PT)v;
+        wave_sync();
       }
-      // j_s == i_t only for s <= t; s == t is the self-swap j_t == i_t, whose predecessor on position
-      // i_t is then pj(t)
-      int pi = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
-      if (pi == lane) pi = pj;
-      int v = P0i, ptr = pi;
-      while (ballot(ptr >= 0)) {
-        const int src = ptr >= 0 ? ptr : lane;
-        const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
-        if (ptr >= 0) { v = v2; ptr = p2; }
-      }
-      const int Vj = __shfl(v, pj >= 0 ? pj : lane);
-      const int F = pj >= 0 ? Vj : P0j;
-      if (acc) perm[i] = (uint16_t)F;
-      if (acc && !((later >> lane) & 1) && !(j >= imin && j < i)) perm[j] = (uint16_t)v;
-      wave_sync();
     }
 #endif
     icur -= nacc;
@@ -272,19 +282,23 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, uint16_t* perm) {
 }
 
 // random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
-__device__ __forceinline__ void floor_shuffle(const Env& e) { mt_randbelow_seq(e, e.S->nf - 1, 1, e.perm()); }
+template <typename PT>
+__device__ __forceinline__ void floor_shuffle_t(const Env& e, PT* perm) { mt_randbelow_seq(e, e.S->nf - 1, 1, perm); }
+__device__ __forceinline__ void floor_shuffle(const Env& e) { floor_shuffle_t(e, e.perm()); }
 
 // Pay the shuffle debt accumulated by membership-only floorlist calls (check_pos_validity, Q3).
-__device__ void pay_debt(const Env& e) {
+template <typename PT>
+__device__ void pay_debt_t(const Env& e, PT* perm) {
 #ifdef MFG_ABLATE_NODEBT
   e.setH(H_DEBT, 0);
   return;
 #endif
   int debt = e.H(H_DEBT);
-  for (int k = 0; k < debt; k++) floor_shuffle(e);
+  for (int k = 0; k < debt; k++) floor_shuffle_t(e, perm);
   e.setH(H_DEBT, 0);
   wave_sync();
 }
+__device__ __forceinline__ void pay_debt(const Env& e) { pay_debt_t(e, e.perm()); }
 
 // CPython random.seed(int) -> init_by_array (Modules/_randommodule.c); serial, once per env
 __device__ void mt_seed(const Env& e, const uint32_t* key, int len) {
@@ -937,8 +951,8 @@ __device__ void env_reset(const Env& e, int* scratch) {
       const bool em = i < nf && lane_cell_empty(e, perm[i < nf ? i : 0]);
       m += popc(ballot(em));
     }
-    const int j = mt_randbelow_seq(e, m - 1, m - 1, nullptr);  // first Fisher-Yates step picks the last slot
-    if (m - 2 >= 1) mt_randbelow_seq(e, m - 2, 1, nullptr);     // remaining draws of shuffle(empty_positions)
+    const int j = mt_randbelow_seq<uint16_t>(e, m - 1, m - 1, nullptr);  // first Fisher-Yates step picks the last slot
+    if (m - 2 >= 1) mt_randbelow_seq<uint16_t>(e, m - 2, 1, nullptr);     // remaining draws of shuffle(empty_positions)
     int k = 0, cell = -1;
     for (int b = 0; b < nf && cell < 0; b += MFG_WAVE) {
       const int i = b + e.lane;
@@ -998,25 +1012,48 @@ __device__ void env_reset(const Env& e, int* scratch) {
 // ------------------------------------------------------------------------------------------------
 // observation (observation_builder.py:138-235, ray_caster.py:66-104)
 // ------------------------------------------------------------------------------------------------
+// Per-env cell map (one byte per grid cell, in LDS), built once per render and shared by all agents:
+// walls come from the static base map, the dynamic entities are OR-ed in. The ray walk reads its
+// light blockers from it and the placement reads each window cell's tag bits with one LDS load.
+#define CM_WALL 1u     // wall (static)
+#define CM_DOOR 2u     // door present in the global pos_dict
+#define CM_DCLOSED 4u  // ... and closed (blocks light, encodes 0.6666)
+#define CM_ITEM 8u
+#define CM_POD 16u
+#define CM_DROP 32u
+#define CM_DEST 64u    // destination present and not reached
+#define CM_DIRT 128u
+
 __device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
   SpecP S = e.S;
   if (x < 0 || y < 0 || x >= S->s.H || y >= S->s.W) return false;
-  const int c = x * S->s.W + y;
-  return (e.light[c >> 5] >> (c & 31)) & 1u;
+  return (e.cmap[x * S->s.W + y] & (CM_WALL | CM_DCLOSED)) != 0;
 }
-// per-env light-blocking bitmap: walls (static) | closed doors present in the global pos_dict
-__device__ void build_light(const Env& e) {
+__device__ __forceinline__ void cmap_or(const Env& e, int cell, uint32_t bit) {
+  atomicOr((uint32_t*)(e.cmap + (cell & ~3)), bit << (8 * (cell & 3)));
+}
+__device__ void build_cmap(const Env& e) {
   SpecP S = e.S;
-  const int nw = (S->HW + 31) >> 5;
-  for (int w = e.lane; w < nw; w += MFG_WAVE) e.light[w] = S->wall_bits[w];
+  const int lane = e.lane;
+  const int n16 = S->map_bytes >> 4;
+  const uint4* src = (const uint4*)S->base_map;
+  for (int i = lane; i < n16; i += MFG_WAVE) ((uint4*)e.cmap)[i] = src[i];
   wave_sync();
-  if (e.lane < S->nd) {
-    const int dw = e.door()[e.lane];
-    if ((dw & DW_PRESENT) && !(dw & DW_OPEN)) {
-      const int c = S->door_cells[e.lane];
-      atomicOr(&e.light[c >> 5], 1u << (c & 31));
-    }
+  if (lane < S->nd) {
+    const int w = e.door()[lane];
+    if (w & DW_PRESENT) cmap_or(e, S->door_cells[lane], CM_DOOR | ((w & DW_OPEN) ? 0u : CM_DCLOSED));
   }
+  auto grp = [&](const int* tbl, int n, uint32_t bit, bool dest) {
+    if (lane < n) {
+      const int w = tbl[lane];
+      if ((w & EW_PRESENT) && EW_POS(w) != EW_NOPOS && !(dest && (w & EW_REACHED))) cmap_or(e, EW_POS(w), bit);
+    }
+  };
+  grp(e.items(), e.H(H_N_ITEMS), CM_ITEM, false);
+  grp(e.pods(), e.H(H_N_PODS), CM_POD, false);
+  grp(e.drops(), e.H(H_N_DROPS), CM_DROP, false);
+  grp(e.dests(), e.H(H_N_DESTS), CM_DEST, true);
+  grp(e.dirtpos(), e.H(H_N_DIRT), CM_DIRT, false);
   wave_sync();
 }
 
@@ -1158,19 +1195,13 @@ __device__ void build_obs(const Env& e, OT* out_env) {
   const int A = S->A, H = S->s.H, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
   const int lane = e.lane;
   const bool frozen = e.H(H_FROZEN) != 0;
-  build_light(e);
+  build_cmap(e);
   int* pairs = e.scratch;
   const int npairs = build_id_pairs(e, pairs);
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
   const int agp = lane < A ? e.agpos()[lane] : -1;
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
-  const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
-  const int itw = lane < nI ? e.items()[lane] : 0;
-  const int pdw = lane < nP ? e.pods()[lane] : 0;
-  const int drw = lane < nR ? e.drops()[lane] : 0;
-  const int dsw = lane < nS ? e.dests()[lane] : 0;
-  const int dtw = lane < nT ? e.dirtpos()[lane] : 0;
-  const double dta = lane < nT ? e.dirtamt()[lane] : 0.0;
+  const int nT = e.H(H_N_DIRT);
   // this lane's ray, loaded once: 16 packed bytes
   RayLane ray;
   {
@@ -1241,52 +1272,52 @@ __device__ void build_obs(const Env& e, OT* out_env) {
         else sup_add(sup, pairs[4 * qq + 2], ca);
       }
     }
-    // ---- placement (lane = window cell): presence bits per tag, values composed per layer ----
+    // ---- placement (lane = window cell): tag bits from the cell map, values composed per layer ----
     const int x = ax - r + wpx, y = ay - r + wpy;
     const bool v = inwin && x >= 0 && y >= 0 && x < H && y < W && ((vis >> lane) & 1);
     const int cell = v ? x * W + y : 0;
-    uint32_t tags = 0;  // bit t = tag t (< 16) has an entity here
-    float door_enc = 0.f;
-    double dirt_amt = 0.0;
-    if (v && ((S->wall_bits[cell >> 5] >> (cell & 31)) & 1u) && !((sup.walls >> lane) & 1)) tags |= 1u << MFG_TAG_WALLS;
-    {
-      const int dI = v ? door_idx(e, cell) : -1;
-      if (dI >= 0) {
-        const int w = e.door()[dI];
-        if ((w & DW_PRESENT) && !((sup.doors >> dI) & 1)) tags |= 1u << MFG_TAG_DOORS;
-        door_enc = (w & DW_OPEN) ? 1.f : 0.f;
+    const uint32_t m = v ? (uint32_t)e.cmap[cell] : 0u;
+    uint32_t tags = 0;  // bit t = tag t (< 16) has a (not suppressed) entity here
+    if ((m & CM_WALL) && !((sup.walls >> lane) & 1)) tags |= 1u << MFG_TAG_WALLS;
+    if (m & CM_DOOR) tags |= 1u << MFG_TAG_DOORS;
+    if (m & CM_ITEM) tags |= 1u << MFG_TAG_ITEMS;
+    if (m & CM_POD) tags |= 1u << MFG_TAG_PODS;
+    if (m & CM_DROP) tags |= 1u << MFG_TAG_DROPOFFS;
+    if (m & CM_DEST) tags |= 1u << MFG_TAG_DESTS;
+    if (m & CM_DIRT) tags |= 1u << MFG_TAG_DIRT;
+    // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
+    if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
+    auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
+      if (!sm) return;
+      bool any = false;
+      for (int i = 0; i < n; i++) {
+        const int w = uni(tbl[i]);
+        any |= v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sm >> i) & 1) && !(dest && (w & EW_REACHED));
       }
+      tags = any ? (tags | (1u << tag)) : (tags & ~(1u << tag));
+    };
+    resup(e.items(), e.H(H_N_ITEMS), sup.items, MFG_TAG_ITEMS, false);
+    resup(e.pods(), e.H(H_N_PODS), sup.pods, MFG_TAG_PODS, false);
+    resup(e.drops(), e.H(H_N_DROPS), sup.drops, MFG_TAG_DROPOFFS, false);
+    resup(e.dests(), e.H(H_N_DESTS), sup.dests, MFG_TAG_DESTS, true);
+    double dirt_amt = 0.0;
+    if (ballot(m & CM_DIRT)) {  // amount of the (last non-suppressed) pile on the cell
+      bool any = false;
+      for (int i = 0; i < nT; i++) {
+        const int w = uni(e.dirtpos()[i]);
+        const double am = e.dirtamt()[i];
+        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) { any = true; dirt_amt = am; }
+      }
+      tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
     }
     u64 amask = 0;
     for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
-    for (int i = 0; i < nI; i++) {
-      const int w = rl(itw, i);
-      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.items >> i) & 1)) tags |= 1u << MFG_TAG_ITEMS;
-    }
-    for (int i = 0; i < nP; i++) {
-      const int w = rl(pdw, i);
-      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.pods >> i) & 1)) tags |= 1u << MFG_TAG_PODS;
-    }
-    for (int i = 0; i < nR; i++) {
-      const int w = rl(drw, i);
-      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.drops >> i) & 1)) tags |= 1u << MFG_TAG_DROPOFFS;
-    }
-    for (int i = 0; i < nS; i++) {
-      const int w = rl(dsw, i);
-      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dests >> i) & 1) && !(w & EW_REACHED))
-        tags |= 1u << MFG_TAG_DESTS;
-    }
-    for (int i = 0; i < nT; i++) {
-      const int w = rl(dtw, i);
-      const double am = rld(dta, i);
-      if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) { tags |= 1u << MFG_TAG_DIRT; dirt_amt = am; }
-    }
-    // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666/0.4444,
-    // dirt = amount); at most one entity per (tag, cell) in the global pos_dict
+    // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
+    // 0.4444 open, dirt = amount)
     auto tagv = [&](int tag) -> double {
       if (tag >= MFG_TAG_AGENT0) return ((amask >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
       if (!((tags >> tag) & 1u)) return 0.0;
-      if (tag == MFG_TAG_DOORS) return door_enc != 0.f ? 0.4444 : 0.6666;
+      if (tag == MFG_TAG_DOORS) return (m & CM_DCLOSED) ? 0.6666 : 0.4444;
       if (tag == MFG_TAG_DIRT) return dirt_amt;
       return 1.0;
     };
@@ -1313,8 +1344,6 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       if (inwin) out_a[(size_t)l * dd + lane] = (OT)val;
     }
   }
-  e.setH(H_OBS_INIT, 1);
-  wave_sync();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1381,40 +1410,45 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
 }
 
 // ------------------------------------------------------------------------------------------------
-// kernels: one wave per env, MFG_WPB waves per workgroup, the env record image in dynamic LDS
+// kernels: one wave per env, MFG_WPB waves per workgroup, (a prefix of) the env record image in
+// dynamic LDS. One env-step is three launches over all envs, each sized for its own working set:
+//   k_logic     actions + rules + rewards/done/events; LDS = record without MT/perm (the "lean" record)
+//               unless the spec consumes the floor order inside a step (dirt spawns)
+//   k_resetdone auto-reset of the envs that just finished (full record, early exit for the rest)
+//   k_obs       observation render; LDS = lean record + cell map + id-collision pairs; read-only on state
+// and k_replay pays the accumulated floor-shuffle debt once per mfg_step call.
 // ------------------------------------------------------------------------------------------------
 #define MFG_WPB 4
 
-__device__ __forceinline__ bool wave_env(SpecP S, uint8_t* smem, long long B, Env& e, long long& env) {
-  const int wid = threadIdx.x >> 6;
-  env = (long long)blockIdx.x * MFG_WPB + wid;
+// full-record slice: [record][scratch 2 KB][shuffle tables]
+__device__ __forceinline__ void env_full(SpecP S, uint8_t* slice, Env& e) {
   e.S = S;
-  e.lds = smem + (size_t)wid * S->lds_per_wave;
-  e.scratch = (int*)(e.lds + S->L.size);
-  e.stab = (uint32_t*)(e.lds + S->L.size + 2048);
-  e.light = e.stab + MFG_STAB_N;
-  e.hdrp = (int*)(e.lds + S->L.o_hdr);
+  e.lds = slice;
+  e.scratch = (int*)(slice + S->L.size);
+  e.stab = (uint32_t*)(slice + S->L.size + 2048);
+  e.cmap = nullptr;
+  e.hdrp = (int*)(slice + S->L.o_hdr);
   e.lane = lane_id();
-  if (env < B) {
-    for (int i = e.lane; i < MFG_STAB_N; i += MFG_WAVE) e.stab[i] = 0u;
-    wave_sync();
-  }
-  return env < B;
+  for (int i = e.lane; i < MFG_STAB_N; i += MFG_WAVE) e.stab[i] = 0u;
+}
+__device__ __forceinline__ void rec_copy(uint8_t* dst, const uint8_t* src, int bytes, int lane) {
+  const int n16 = bytes >> 4;
+  for (int i = lane; i < n16; i += MFG_WAVE) ((uint4*)dst)[i] = ((const uint4*)src)[i];
 }
 
-// creation (init=1): random.seed(py_seed), Factory.__init__ (floor list, OBSBuilder shuffle); then reset
-template <int MAXPTS, typename OT>
+// creation (init=1): random.seed(py_seed), Factory.__init__ (floor list, OBSBuilder shuffle); then reset.
+// The first observation is rendered by k_obs afterwards.
 __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, uint8_t* state, long long B,
-                                                        const uint8_t* mask, OT* obs, int init,
-                                                        unsigned long long seed_base) {
+                                                        const uint8_t* mask, int init, unsigned long long seed_base) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
-  Env e;
-  long long env;
-  if (!wave_env(S, smem, B, e, env)) return;
+  const int wid = threadIdx.x >> 6;
+  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  if (env >= B) return;
   if (mask && !mask[env]) return;
+  Env e;
+  env_full(S, smem + (size_t)wid * S->lds_full, e);
   uint8_t* rec = state + (size_t)env * S->L.size;
-  int* scratch = e.scratch;
   if (init) {
     for (int i = e.lane; i < (S->L.size >> 2); i += MFG_WAVE) ((int*)e.lds)[i] = 0;
     wave_sync();
@@ -1436,16 +1470,103 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, ui
     wave_sync();
     floor_shuffle(e);  // OBSBuilder.__init__: `for pos in state.entities.floorlist` (observation_builder.py:57)
   } else {
-    rec_load(e, rec);
+    rec_copy(e.lds, rec, S->L.size, e.lane);
+    wave_sync();
   }
-  env_reset(e, scratch);
-  if (obs) build_obs<MAXPTS, OT>(e, obs + (size_t)env * S->A * S->obs_agent_stride);
-  else e.setH(H_OBS_INIT, 1);
-  rec_store(e, rec);
+  env_reset(e, e.scratch);
+  e.setH(H_OBS_INIT, 1);  // the reference renders right after every reset
+  e.setH(H_DONE, 0);
+  wave_sync();
+  rec_copy(rec, e.lds, S->L.size, e.lane);
+}
+
+// One env-step of every env (no reset, no render).
+__global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, uint8_t* state, long long B,
+                                                        const int32_t* actions, unsigned philox_seed,
+                                                        unsigned env_base, long long step, double* reward,
+                                                        uint8_t* done, uint8_t* ev_act, uint8_t* ev_watch,
+                                                        int32_t* ev_misc, int auto_reset) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const int wid = threadIdx.x >> 6;
+  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  if (env >= B) return;
+  Env e;
+  uint8_t* slice = smem + (size_t)wid * S->lds_logic;
+  const bool full = S->step_rng != 0;
+  if (full) {
+    env_full(S, slice, e);
+  } else {
+    e.S = S; e.lds = slice; e.scratch = nullptr; e.stab = nullptr; e.cmap = nullptr;
+    e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
+  }
+  uint8_t* rec = state + (size_t)env * S->L.size;
+  const int bytes = full ? S->L.size : S->L.o_mt;
+  rec_copy(e.lds, rec, bytes, e.lane);
+  wave_sync();
+  const int A = S->A;
+  int my_act = 0;
+  if (e.lane < A) {
+    if (actions) {
+      my_act = actions[(size_t)env * A + e.lane];
+    } else {
+      const uint32_t u = philox_u32(philox_seed, env_base + (uint32_t)env, (uint32_t)step, (uint32_t)e.lane);
+      my_act = (int)(((uint64_t)u * (uint64_t)S->s.n_actions[e.lane]) >> 32);
+    }
+  }
+  StepOut o;
+  env_step(e, my_act, o, e.scratch);
+  write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
+  if (o.done && auto_reset) e.setH(H_DONE, 1);
+  wave_sync();
+  rec_copy(rec, e.lds, bytes, e.lane);
+}
+
+// Auto-reset of the envs k_logic flagged (H_DONE): pays the shuffle debt, then Factory.reset().
+__global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const int wid = threadIdx.x >> 6;
+  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  if (env >= B) return;
+  uint8_t* rec = state + (size_t)env * S->L.size;
+  if (uni(((const int*)(rec + S->L.o_hdr))[H_DONE]) == 0) return;
+  Env e;
+  env_full(S, smem + (size_t)wid * S->lds_full, e);
+  rec_copy(e.lds, rec, S->L.size, e.lane);
+  wave_sync();
+  env_reset(e, e.scratch);
+  e.setH(H_DONE, 0);
+  wave_sync();
+  rec_copy(rec, e.lds, S->L.size, e.lane);
+}
+
+// Observation render of every env into obs[env] (read-only on the state).
+template <int MAXPTS, typename OT>
+__global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
+                                                      OT* obs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const int wid = threadIdx.x >> 6;
+  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  if (env >= B) return;
+  // slice: [lean record][cell map][pairs]
+  uint8_t* slice = smem + (size_t)wid * S->lds_obs;
+  Env e;
+  e.S = S; e.lds = slice; e.stab = nullptr;
+  e.cmap = slice + S->L.o_mt;
+  e.scratch = (int*)(slice + S->L.o_mt + S->map_bytes);
+  e.hdrp = (int*)(slice + S->L.o_hdr);
+  e.lane = lane_id();
+  const uint8_t* rec = state + (size_t)env * S->L.size;
+  rec_copy(e.lds, rec, S->L.o_mt, e.lane);
+  wave_sync();
+  build_obs<MAXPTS, OT>(e, obs + (size_t)env * S->A * S->obs_agent_stride);
+  if (e.lane == 0 && e.hdrp[H_OVERFLOW]) ((int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_OVERFLOW] = 1;
 }
 
 // Pay every env's pending floor-shuffle debt. Touches only the header, MT state and floor permutation
-// of each record (the obs/step state stays in HBM), so it runs at high occupancy.
+// of each record, so it runs at high occupancy.
 __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, uint8_t* state, long long B) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
@@ -1461,68 +1582,39 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   e.lds = smem + (size_t)wid * S->lds_replay_per_wave - S->L.o_mt + 4 * MFG_HDR_N;
   e.lane = lane_id();
   e.scratch = nullptr;
-  e.light = nullptr;
-  e.stab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_jtab_off);
+  e.cmap = nullptr;
+  e.stab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_stab_off);
   e.hdrp = (int*)(smem + (size_t)wid * S->lds_replay_per_wave);
   int* hdr = e.hdr();
-  const int nmt = (S->L.o_perm + 2 * S->nf - S->L.o_mt + 15) >> 4;  // MT + perm bytes, 16 B units
-  // header: lanes copy 32 ints; MT + perm: 16 B per lane
+  uint32_t* p32 = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_perm_off);
+  const int nf = S->nf;
+  // header: lanes copy 32 ints; MT: 16 B per lane; perm: u16 pairs widened to u32
   if (e.lane < MFG_HDR_N) hdr[e.lane] = ((const int*)(rec + S->L.o_hdr))[e.lane];
   {
     const uint4* src = (const uint4*)(rec + S->L.o_mt);
     uint4* dst = (uint4*)(e.lds + S->L.o_mt);
-    for (int i = e.lane; i < nmt; i += MFG_WAVE) dst[i] = src[i];
+    for (int i = e.lane; i < 624 / 4; i += MFG_WAVE) dst[i] = src[i];
+    const uint32_t* ps = (const uint32_t*)(rec + S->L.o_perm);
+    for (int i = e.lane; 2 * i < nf; i += MFG_WAVE) {
+      const uint32_t w = ps[i];
+      p32[2 * i] = w & 0xFFFFu;
+      p32[2 * i + 1] = w >> 16;
+    }
   }
-  for (int i = e.lane; i < MFG_STAB_N; i += MFG_WAVE) e.stab[i] = 0u;
+  for (int i = e.lane; i < S->replay_stab_n; i += MFG_WAVE) e.stab[i] = 0u;
   wave_sync();
-  pay_debt(e);
+  pay_debt_t(e, p32);
   {
     const uint4* src = (const uint4*)(e.lds + S->L.o_mt);
     uint4* dst = (uint4*)(rec + S->L.o_mt);
-    for (int i = e.lane; i < nmt; i += MFG_WAVE) dst[i] = src[i];
+    for (int i = e.lane; i < 624 / 4; i += MFG_WAVE) dst[i] = src[i];
+    uint32_t* pd = (uint32_t*)(rec + S->L.o_perm);
+    for (int i = e.lane; 2 * i < nf; i += MFG_WAVE) pd[i] = (p32[2 * i] & 0xFFFFu) | (p32[2 * i + 1] << 16);
   }
   if (e.lane == 0) {
     ((int*)(rec + S->L.o_hdr))[H_DEBT] = 0;
     ((int*)(rec + S->L.o_hdr))[H_MT_IDX] = hdr[H_MT_IDX];
   }
-}
-
-template <int MAXPTS, typename OT>
-__global__ void __launch_bounds__(MFG_WPB * 64) k_step(const MfgDevSpec* S_, uint8_t* state, long long B, int K,
-                                                       const int32_t* actions, unsigned philox_seed,
-                                                       unsigned env_base, long long step_base, double* reward, uint8_t* done, OT* obs,
-                                                       uint8_t* ev_act, uint8_t* ev_watch, int32_t* ev_misc,
-                                                       int auto_reset) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  SpecP S = (SpecP)S_;
-  Env e;
-  long long env;
-  if (!wave_env(S, smem, B, e, env)) return;
-  uint8_t* rec = state + (size_t)env * S->L.size;
-  int* scratch = e.scratch;
-  const int A = S->A;
-  rec_load(e, rec);
-  for (int k = 0; k < K; k++) {
-    const size_t row = (size_t)k * B + env;
-    int my_act = 0;
-    if (e.lane < A) {
-      if (actions) {
-        my_act = actions[row * A + e.lane];
-      } else {
-        const uint32_t u = philox_u32(philox_seed, env_base + (uint32_t)env, (uint32_t)(step_base + k),
-                                    (uint32_t)e.lane);
-        my_act = (int)(((uint64_t)u * (uint64_t)S->s.n_actions[e.lane]) >> 32);
-      }
-    }
-    StepOut o;
-    env_step(e, my_act, o, scratch);
-    write_step_outputs(e, o, row, reward, done, ev_act, ev_watch, ev_misc);
-    if (o.done && auto_reset) env_reset(e, scratch);
-#ifndef MFG_ABLATE_NOOBS
-    if (obs) build_obs<MAXPTS, OT>(e, obs + row * A * S->obs_agent_stride);
-#endif
-  }
-  rec_store(e, rec);
 }
 
 // ================================================================================================
@@ -1619,9 +1711,52 @@ static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int
   L->o_frozen_bat = o; o += 8 * A;
   L->o_dirt_amt = o; o += 8 * dm;
   L->o_pcg = o; o += 8 * 4;
+  o = align_up(o, 16);
   L->o_mt = o; o += 4 * 624;
   L->o_perm = o; o += 2 * s->n_floor;
   L->size = align_up(o, 16);
+}
+
+// Probe: does one ds_wrxchg with conflicting addresses apply its lanes in ascending lane order (each
+// lane gets the previous same-address lane's value back, the last lane's value stays)? The exchange
+// path of the shuffle blocks relies on it; without it the table path is used.
+__global__ void __launch_bounds__(64) k_probe_xchg(int* bad) {
+  __shared__ uint32_t tab[64];
+  const int lane = lane_id();
+  int nbad = 0;
+  for (int it = 1; it <= 64; it++) {
+    tab[lane] = 1000u + lane;
+    wave_sync();
+    const int a = (int)((lane * 2654435761u + it * 40503u) >> 7) % it;  // many conflicts, varied patterns
+    const uint32_t old = atomicExch(&tab[a], (uint32_t)lane);
+    wave_sync();
+    // expected: the previous lane with the same address, or the initial value
+    int prev = -1;
+    for (int l = 0; l < lane; l++)
+      if ((int)((l * 2654435761u + it * 40503u) >> 7) % it == a) prev = l;
+    const uint32_t want = prev >= 0 ? (uint32_t)prev : 1000u + a;
+    int last = -1;
+    for (int l = 0; l < 64; l++)
+      if ((int)((l * 2654435761u + it * 40503u) >> 7) % it == lane) last = l;
+    const uint32_t want_fin = last >= 0 ? (uint32_t)last : 1000u + lane;
+    nbad += (old != want) + (tab[lane] != want_fin);
+    wave_sync();
+  }
+  atomicAdd(bad, nbad);
+}
+
+static int probe_xchg_order(int device) {
+  if (const char* f = getenv("MFG_SHUFFLE_TABLE_PATH")) if (f[0] == '1') return 0;
+  (void)device;
+  int* d = nullptr;
+  int h = -1;
+  if (hipMalloc((void**)&d, sizeof(int)) != hipSuccess) return 0;
+  if (hipMemset(d, 0, sizeof(int)) == hipSuccess) {
+    hipLaunchKernelGGL(k_probe_xchg, dim3(1), dim3(64), 0, 0, d);
+    if (hipMemcpy(&h, d, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) h = -1;
+  }
+  (void)hipFree(d);
+  return h == 0 ? 1 : 0;
 }
 
 extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out) {
@@ -1658,20 +1793,28 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   if (imax > 64 || pmax > 64 || dropmax > 64 || destmax > 64) { delete e; return fail("group quantity > 64"); }
   h.imax = imax; h.pmax = pmax; h.dropmax = dropmax; h.destmax = destmax;
   make_layout(s, &h.L, imax, pmax, dropmax, destmax);
-  h.lds_per_wave = align_up(h.L.size + 2048 + 4 * MFG_STAB_N + 4 * ((HW + 31) / 32), 16);
+  h.step_rng = 0;
+  for (int r = 0; r < s->n_rules; r++)
+    if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT) h.step_rng = 1;  // dirt spawns pay the debt mid-step
+  h.map_bytes = align_up(HW, 16);
+  h.lds_full = align_up(h.L.size + 2048 + 4 * MFG_STAB_N, 16);
+  h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
+  h.lds_obs = align_up(h.L.o_mt, 16) + h.map_bytes + 16 * OBS_MAX_PAIRS;
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
-    const int mtperm = align_up(h.L.o_perm + 2 * h.nf - h.L.o_mt, 16);
-    h.replay_jtab_off = 4 * MFG_HDR_N + mtperm;
-    h.lds_replay_per_wave = align_up(h.replay_jtab_off + 4 * MFG_STAB_N, 16);
+    h.xchg_ordered = probe_xchg_order(device);
+    h.replay_perm_off = 4 * MFG_HDR_N + 4 * 624;
+    h.replay_stab_off = h.replay_perm_off + align_up(4 * (h.nf + 1), 16);
+    h.replay_stab_n = h.xchg_ordered ? MFG_STAB_PTAB : MFG_STAB_N;
+    h.lds_replay_per_wave = align_up(h.replay_stab_off + 4 * h.replay_stab_n, 16);
   }
   pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
   // static tables
   std::vector<uint8_t> door_of(HW, 0xFF);
   for (int d = 0; d < s->n_doors; d++) door_of[s->door_cells[d]] = (uint8_t)d;
-  std::vector<uint32_t> wall_bits((HW + 31) / 32, 0u);
+  std::vector<uint8_t> base_map(h.map_bytes, 0);
   for (int c = 0; c < HW; c++)
-    if (s->level[c] == 1) wall_bits[c >> 5] |= 1u << (c & 31);
+    if (s->level[c] == 1) base_map[c] = CM_WALL;
   std::vector<int32_t> wd;
   const int reach = 2 * s->pomdp_r + 1;
   for (int k = 0; k < s->n_walls && k < s->n_doors; k++) {
@@ -1701,7 +1844,7 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   rc |= upload(e, s->floor_cells, s->n_floor, &h.floor_init);
   rc |= upload(e, rp.data(), rp.size(), &h.ray_pts);
   rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
-  rc |= upload(e, wall_bits.data(), wall_bits.size(), &h.wall_bits);
+  rc |= upload(e, base_map.data(), base_map.size(), &h.base_map);
   rc |= upload(e, wd.data(), wd.size(), &h.wd_pairs);
   if (rc) { delete e; return -1; }
   if (hipMalloc((void**)&e->d_spec, sizeof(MfgDevSpec)) != hipSuccess ||
@@ -1726,13 +1869,14 @@ extern "C" int mfg_destroy(mfg_engine* e) {
   return 0;
 }
 
-// record layout for host-side decoding (tests, snapshots): [size, o_hdr, ..., o_perm, lmax, obs_agent_stride]
+// record layout for host-side decoding (tests, snapshots):
+// [size, o_hdr, ..., o_perm, lmax, obs_agent_stride, lds_full, xchg_ordered]
 extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
   const MfgLayout& L = e->h.L;
   const int32_t v[] = {L.size, L.o_hdr, L.o_rule_ctr, L.o_agent_pos, L.o_agent_arr, L.o_agent_par, L.o_frozen_org,
                        L.o_frozen_gp, L.o_door, L.o_items, L.o_pods, L.o_drops, L.o_dests, L.o_dirt_pos,
                        L.o_dirt_id, L.o_battery, L.o_frozen_bat, L.o_dirt_amt, L.o_pcg, L.o_mt, L.o_perm,
-                       e->h.lmax, e->h.obs_agent_stride, e->h.lds_per_wave};
+                       e->h.lmax, e->h.obs_agent_stride, e->h.lds_full, e->h.xchg_ordered};
   const int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
@@ -1740,24 +1884,12 @@ extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
 
 extern "C" void* mfg_state_ptr(mfg_engine* e) { return e ? e->d_state : nullptr; }
 
+static unsigned env_grid(const mfg_engine* e) { return (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB); }
+
 template <int MP, typename OT>
-static hipError_t launch_reset_t(mfg_engine* e, const uint8_t* mask, OT* obs, int init, unsigned long long seed_base,
-                                 hipStream_t st) {
-  const unsigned grid = (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB);
-  const size_t lds = (size_t)e->h.lds_per_wave * MFG_WPB;
-  hipLaunchKernelGGL((k_reset<MP, OT>), dim3(grid), dim3(MFG_WPB * 64), lds, st, e->d_spec, e->d_state,
-                     (long long)e->B, mask, obs, init, seed_base);
-  return hipGetLastError();
-}
-template <int MP, typename OT>
-static hipError_t launch_step_t(mfg_engine* e, int K, const int32_t* actions, unsigned seed, unsigned env_base,
-                                long long step_base, double* reward, uint8_t* done, OT* obs, uint8_t* ev_act,
-                                uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, hipStream_t st) {
-  const unsigned grid = (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB);
-  const size_t lds = (size_t)e->h.lds_per_wave * MFG_WPB;
-  hipLaunchKernelGGL((k_step<MP, OT>), dim3(grid), dim3(MFG_WPB * 64), lds, st, e->d_spec, e->d_state,
-                     (long long)e->B, K, actions, seed, env_base, step_base, reward, done, obs, ev_act, ev_watch,
-                     ev_misc, auto_reset);
+static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
+  hipLaunchKernelGGL((k_obs<MP, OT>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_obs * MFG_WPB, st,
+                     e->d_spec, e->d_state, (long long)e->B, obs);
   return hipGetLastError();
 }
 
@@ -1769,55 +1901,76 @@ static hipError_t launch_step_t(mfg_engine* e, int K, const int32_t* actions, un
     default: return fail("unsupported ray length"); \
   }
 
-// reset (init=1: create envs, seeding env i with random.seed(seed_base + i)); obs_dtype 0=f32 1=f64
-extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init,
-                         uint64_t seed_base, void* stream) {
-  if (!e) return fail("null engine");
+// render obs of every env into obs (obs_dtype 0 = f32, 1 = f64)
+static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st) {
   hipError_t err = hipSuccess;
-  hipStream_t st = (hipStream_t)stream;
   if (obs_dtype == 1) {
-    DISPATCH_MP(e->maxpts, err = (launch_reset_t<MP, double>(e, mask, (double*)obs, init, seed_base, st)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double>(e, (double*)obs, st)));
   } else {
-    DISPATCH_MP(e->maxpts, err = (launch_reset_t<MP, float>(e, mask, (float*)obs, init, seed_base, st)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float>(e, (float*)obs, st)));
   }
-  if (err != hipSuccess) return fail(std::string("k_reset launch: ") + hipGetErrorString(err));
+  if (err != hipSuccess) return fail(std::string("k_obs launch: ") + hipGetErrorString(err));
   return 0;
 }
 
-// K fused steps. actions: device [K][B][A] int32, or NULL -> Philox4x32-10 synthetic actions keyed
-// (philox_seed, env_base+env) at counter (step_base+k, agent). Outputs (each may be NULL):
-// reward [K][B][A] f64, done [K][B] u8, obs [K][B][A][lmax][d][d], ev_act/ev_watch [K][B][A] u8,
-// ev_misc [K][B][10] i32. auto_reset: envs that finish are reset in-kernel (the obs row is then the
-// first observation of the new episode).
+// reset (init=1: create envs, seeding env i with random.seed(seed_base + i)); obs_dtype 0=f32 1=f64.
+// With a mask only the masked envs are reset, but obs (if given) is rendered for every env.
+extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init,
+                         uint64_t seed_base, void* stream) {
+  if (!e) return fail("null engine");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_reset, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_full * MFG_WPB, st, e->d_spec,
+                     e->d_state, (long long)e->B, mask, init, (unsigned long long)seed_base);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return fail(std::string("k_reset launch: ") + hipGetErrorString(err));
+  return obs ? launch_obs(e, obs, obs_dtype, st) : 0;
+}
+
 // Pay all pending floor-shuffle debt (membership-only shuffles of the reference's move checks, Q3).
 extern "C" int mfg_replay(mfg_engine* e, void* stream) {
   if (!e) return fail("null engine");
-  const unsigned grid = (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB);
   const size_t lds = (size_t)e->h.lds_replay_per_wave * MFG_WPB;
-  hipLaunchKernelGGL(k_replay, dim3(grid), dim3(MFG_WPB * 64), lds, (hipStream_t)stream, e->d_spec, e->d_state,
+  hipLaunchKernelGGL(k_replay, dim3(env_grid(e)), dim3(MFG_WPB * 64), lds, (hipStream_t)stream, e->d_spec, e->d_state,
                      (long long)e->B);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
   return 0;
 }
 
+// K steps. actions: device [K][B][A] int32, or NULL -> Philox4x32-10 synthetic actions keyed
+// (philox_seed, env_base+env) at counter (step_base+k, agent). Outputs (each may be NULL):
+// reward [K][B][A] f64, done [K][B] u8, obs [K][B][A][lmax][d][d], ev_act/ev_watch [K][B][A] u8,
+// ev_misc [K][B][10] i32. auto_reset: envs that finish are reset (the obs row is then the first
+// observation of the new episode). Per step: k_logic, k_resetdone (auto_reset), k_obs (obs); then one
+// k_replay for the whole call.
 extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
                         int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype,
                         uint8_t* ev_act, uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
   if (!e) return fail("null engine");
   if (K < 1) return fail("K must be >= 1");
-  hipError_t err = hipSuccess;
   hipStream_t st = (hipStream_t)stream;
-  if (obs_dtype == 1) {
-    DISPATCH_MP(e->maxpts, err = (launch_step_t<MP, double>(e, K, actions, philox_seed, env_base, step_base, reward,
-                                                            done, (double*)obs, ev_act, ev_watch, ev_misc,
-                                                            auto_reset, st)));
-  } else {
-    DISPATCH_MP(e->maxpts, err = (launch_step_t<MP, float>(e, K, actions, philox_seed, env_base, step_base, reward,
-                                                           done, (float*)obs, ev_act, ev_watch, ev_misc, auto_reset,
-                                                           st)));
+  const size_t B = (size_t)e->B, A = (size_t)e->h.A;
+  const size_t obs_row = B * A * (size_t)e->h.obs_agent_stride * (obs_dtype == 1 ? 8 : 4);
+  for (int k = 0; k < K; k++) {
+    const size_t kb = (size_t)k * B;
+    hipLaunchKernelGGL(k_logic, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
+                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
+                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
+                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
+                       auto_reset);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return fail(std::string("k_logic launch: ") + hipGetErrorString(err));
+    if (auto_reset) {
+      hipLaunchKernelGGL(k_resetdone, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_full * MFG_WPB, st,
+                         e->d_spec, e->d_state, (long long)e->B);
+      err = hipGetLastError();
+      if (err != hipSuccess) return fail(std::string("k_resetdone launch: ") + hipGetErrorString(err));
+    }
+#ifndef MFG_ABLATE_NOOBS
+    if (obs && launch_obs(e, (uint8_t*)obs + (size_t)k * obs_row, obs_dtype, st)) return -1;
+#endif
   }
-  if (err != hipSuccess) return fail(std::string("k_step launch: ") + hipGetErrorString(err));
   return mfg_replay(e, stream);
 }
 
