@@ -2,14 +2,21 @@
 """bench.py — env-steps/sec of the MI355X batched step engine on the headline workload.
 
 Workload (BASELINE.json configs[2]): 'large' level, 8 agents, doors + items + batteries,
-B = 65536 envs per GPU, synthetic uniform random actions (Philox4x32-10 on the device), auto-reset with
-reference reset semantics, dense fp32 observations (8 agents x 7 layers x 7x7) written to HBM every step,
-f64 rewards, done flags and info events. One "step" = one env-step of every env on every GPU.
+B = 65536 envs per GPU, synthetic uniform random actions (Philox4x32-10 on the device, keyed (seed, env)
+at counter (step, agent)), auto-reset with reference reset semantics, dense fp32 observations
+(8 agents x 7 layers x 7x7) written to HBM every step, f64 rewards, done flags and info events.
+One "step" = one env-step of every env on every GPU. Measurement protocol of SURVEY §8(d): >= 600
+warm-up steps (every env has passed episode 1, Q11/Q12 active), then >= 2000 timed steps; with
+500-step episodes the timed window holds the resets in proportion.
 
-Timed region: exactly --steps steps (fused into launches of --fuse steps), bracketed by barrier +
+Timed region: exactly --steps steps (mfg_step calls of --fuse steps), bracketed by barrier +
 torch.cuda.synchronize() on both sides, max over ranks. value = all envs x steps / max time.
-roofline: the step kernel's algorithmic bytes (11,391 B per env-step, fp32 obs) per
-launch / its mean launch time measured with HIP events on the launch stream; peak 8 TB/s (HBM3E).
+
+roofline: per-kernel HIP events recorded by the engine around each launch on the launch stream
+(mfg_profile) over the timed region. Top level = the dominant kernel (largest share of time) with its
+algorithmic bytes per launch; "pipeline" = the whole step against SURVEY §8(d)'s
+11,391 B per env-step; "kernels" = every kernel's share. traffic = HBM bytes per launch of the dominant
+kernel from the committed rocprofv3 PMC summary (profiles/pmc_*.json, FETCH_SIZE x2 + WRITE_SIZE).
 cpu_baseline: the C restatement (oracle/, kind "port") on this host's cores, same config and actions,
 bounded sample. Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`,
 one rank per GPU, env ranges sharded (weak scaling), no collective in the data path.
@@ -31,8 +38,20 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "env-steps/sec (whole node), 8-agent 'large' level, batch 65536, 1/2/4/8 MI355X"
 
 
+def algo_bytes(kernel, spec, obs_bytes_per_env, k_launch):
+    """Algorithmic (minimal) bytes one launch of `kernel` moves per env."""
+    core = 415 if spec.n_agents == 8 else None  # SURVEY §8(d) canonical SoA, C3
+    if kernel == 'k_logic':
+        return core
+    if kernel == 'k_obs':
+        return obs_bytes_per_env + 230  # obs written once + mutable/constant state read once
+    if kernel == 'k_replay':
+        return 2 * (4 * 624 + 2 * spec.c.n_floor)  # MT state + floor permutation, read + written
+    return None
+
+
 def cpu_baseline(config, seconds, workers, seed):
-    """Time the C port (oracle) on host cores: `workers` processes, each stepping its own envs."""
+    """Time the C port (oracle) on host cores: `workers` processes, each stepping its own env."""
     import multiprocessing as mp
     ctx = mp.get_context('fork')
     q = ctx.Queue()
@@ -48,12 +67,12 @@ def cpu_baseline(config, seconds, workers, seed):
 
 
 def _cpu_worker(config, seconds, seed, w, q):
-    import numpy as np
+    import numpy as np  # noqa: F401
     import oracle as O
     from philox import synthetic_actions
     from mfg_amd.spec import compile_spec
     spec = compile_spec(config)
-    env = O.OracleEnv(spec, 10_000_000 + w)
+    env = O.OracleEnv(spec, w)
     env.reset()
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -66,14 +85,24 @@ def _cpu_worker(config, seconds, seed, w, q):
     q.put((n, time.perf_counter() - t0))
 
 
-def load_pmc(config_tag):
-    """HBM traffic per step-kernel launch from the committed rocprofv3 PMC summary (profiles/)."""
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def load_pmc(workload):
+    """HBM traffic per launch from the committed rocprofv3 PMC summary (profiles/pmc_*.json)."""
     for p in sorted((ROOT / 'profiles').glob('pmc_*.json'), reverse=True):
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
-        if d.get('workload') == config_tag:
+        if d.get('workload') == workload:
             return d
     return None
 
@@ -81,14 +110,15 @@ def load_pmc(config_tag):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=200)
-    ap.add_argument('--warmup', type=int, default=40)
-    ap.add_argument('--fuse', type=int, default=8, help='env-steps fused per kernel launch')
+    ap.add_argument('--steps', type=int, default=2000)
+    ap.add_argument('--warmup', type=int, default=600)
+    ap.add_argument('--fuse', type=int, default=8, help='env-steps per mfg_step call (one k_replay per call)')
     ap.add_argument('--batch', type=int, default=65536, help='envs per GPU')
     ap.add_argument('--config', default='large8.yaml')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--cpu-workers', type=int, default=0, help='0 = min(16, host cores)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-profile', action='store_true', help='no per-kernel HIP events in the timed region')
     args = ap.parse_args()
 
     import torch
@@ -102,12 +132,13 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from mfg_amd.spec import compile_spec
     from mfg_amd.engine import Engine
+    from mfg_amd.shard import env_range
 
     spec = compile_spec(args.config)
     B, A, F = args.batch, spec.n_agents, args.fuse
     dev = torch.device('cuda', local)
     eng = Engine(spec, B, device=local)
-    env_base = rank * B
+    env_base, _ = env_range(rank, world, B)
     obs = torch.zeros((F,) + eng.obs_shape(), dtype=torch.float32, device=dev)
     rew = torch.zeros((F, B, A), dtype=torch.float64, device=dev)
     done = torch.zeros((F, B), dtype=torch.uint8, device=dev)
@@ -117,6 +148,7 @@ def main():
     eng.reset(obs=obs[0], init=True, seed_base=env_base)
     stream = torch.cuda.current_stream(dev)
     step_no = 0
+    episodes = torch.zeros((), dtype=torch.float64, device=dev)
 
     def run(n, events=None):
         nonlocal step_no
@@ -139,52 +171,89 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    launches = []
+    calls = []
+    eng.profile(not args.no_profile)
+    eng.profile_read()
     t0 = time.perf_counter()
-    run(args.steps, launches)
+    run(args.steps, calls)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    full = [(s.elapsed_time(e) * 1e-3, k) for s, e, k in launches if k == F] or \
-           [(s.elapsed_time(e) * 1e-3, k) for s, e, k in launches]
-    mean_launch = sum(t for t, _ in full) / len(full)
-    k_launch = full[0][1]
+    prof = eng.profile_read()
+    eng.profile(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        m = torch.tensor([float(done[:].sum().item())], dtype=torch.float64, device=dev)
-        dist.all_reduce(m)  # optional metrics all-reduce (tiny, latency-bound)
+        episodes += done.double().sum()
+        dist.all_reduce(episodes)  # optional metrics all-reduce (tiny, latency-bound)
     total = B * world * args.steps
     value = total / elapsed
     if rank == 0:
-        algo = ALGO_BYTES_PER_ENV_STEP * B * k_launch
-        achieved = algo / mean_launch / 1e9
-        pmc = load_pmc('large8_b65536') if args.config == 'large8.yaml' and B == 65536 else None
+        full = [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls if k == F] or \
+               [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls]
+        mean_call = sum(t for t, _ in full) / len(full)
+        k_call = full[0][1]
+        obs_bytes = A * spec.n_layers[0] * spec.d * spec.d * 4 if len(set(spec.n_layers)) == 1 else \
+            sum(spec.n_layers[a] for a in range(A)) * spec.d * spec.d * 4
+        busy = sum(ms for ms, n in prof.values())
+        kernels = {}
+        for name, (ms, n) in prof.items():
+            if not n:
+                continue
+            mean_ms = ms / n
+            ab = algo_bytes(name, spec, obs_bytes, k_call)
+            per_launch = None
+            if ab is not None:
+                units = B * (k_call if name == 'k_replay' else 1)
+                per_launch = ab * (B if name == 'k_replay' else units)
+            kernels[name] = {"launches": n, "mean_launch_ms": round(mean_ms, 4),
+                             "share": round(ms / busy, 4) if busy else None,
+                             "algo_bytes_per_launch": per_launch,
+                             "achieved_GBs": round(per_launch / (mean_ms * 1e-3) / 1e9, 2) if per_launch else None}
+        dom = max(kernels, key=lambda k: prof[k][0]) if kernels else None
+        workload = f"{Path(args.config).stem}_b{B}_f{F}"
+        pmc = load_pmc(workload)
         traffic = None
-        if pmc and pmc.get('fuse') == k_launch:
-            traffic = pmc.get('hbm_bytes_per_launch')
+        if pmc and dom and dom in pmc.get('hbm_bytes_per_launch', {}):
+            traffic = pmc['hbm_bytes_per_launch'][dom]
+        pipe_bytes = ALGO_BYTES_PER_ENV_STEP * B * k_call
+        if dom:
+            dk = kernels[dom]
+            achieved = dk["achieved_GBs"]
+            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
+                    "kernel": dom, "mean_launch_ms": dk["mean_launch_ms"],
+                    "algo_bytes_per_launch": dk["algo_bytes_per_launch"],
+                    "pipeline": {"algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
+                                 "env_steps_per_call": B * k_call, "mean_call_ms": round(mean_call * 1e3, 3),
+                                 "achieved": round(pipe_bytes / mean_call / 1e9, 2),
+                                 "frac": round(pipe_bytes / mean_call / 1e9 / HBM_PEAK_GBS, 5)},
+                    "kernels": kernels}
+        else:
+            roof = {"bound": "hbm", "achieved": round(pipe_bytes / mean_call / 1e9, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(pipe_bytes / mean_call / 1e9 / HBM_PEAK_GBS, 5),
+                    "traffic": None, "kernel": "mfg_step pipeline", "mean_launch_ms": round(mean_call * 1e3, 3)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))
             v, n, wall = cpu_baseline(args.config, args.cpu_seconds, workers, 12345)
             cpu = {"value": round(v, 1), "unit": "env-steps/s", "cores": workers, "kind": "port",
-                   "sample": f"{n} env-steps of {args.config} (obs incl.) on {workers} processes x "
-                             f"{wall:.1f}s, C restatement oracle/mfg_oracle.c"}
+                   "sample": f"{n} env-steps of {args.config} (obs incl., auto-reset) on {workers} processes x "
+                             f"{wall:.1f}s, C restatement oracle/mfg_oracle.c, 1 env per process, "
+                             f"{len(os.sched_getaffinity(0))} cores visible, {cpu_model()}"}
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (Philox4x32-10 uniform random actions, device-side)",
-            "config": {"workload": "C3 large8: 'large' level, 8 agents, doors+items+batteries, pomdp_r 3",
-                       "envs_per_gpu": B, "global_batch": B * world, "obs": "dense fp32 [8,7,7,7] per env-step",
+            "config": {"workload": f"C3 {Path(args.config).stem}: 'large' level, 8 agents, doors+items+batteries, "
+                                   f"pomdp_r 3" if args.config == 'large8.yaml' else Path(args.config).stem,
+                       "envs_per_gpu": B, "global_batch": B * world, "obs": "dense fp32 per env-step",
                        "fuse": F, "auto_reset": True, "parallelism": f"env-shard x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "k_step", "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
-                         "mean_launch_ms": round(mean_launch * 1e3, 3), "env_steps_per_launch": B * k_launch},
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

@@ -196,8 +196,9 @@ int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int 
  * actions from Philox4x32-10 keyed (philox_seed, env_base + b) at counter (step_base + k, agent).
  * Outputs (device, each may be NULL): reward f64 [K][B][A], done u8 [K][B], obs [K][B][A][lmax][d][d],
  * ev_act / ev_watch u8 [K][B][A] and ev_misc i32 [K][B][10] (the info-dict event record).
- * auto_reset != 0: an env whose step is done is reset in the same launch; its obs row is then the new
- * episode's first observation. Pending floor-shuffle debt is replayed (mfg_replay) before returning. */
+ * auto_reset != 0: an env whose step is done is reset before its obs row is rendered, so the row is the
+ * new episode's first observation. Per step the engine launches k_logic, k_resetdone (auto_reset) and
+ * k_obs (obs != NULL); pending floor-shuffle debt is replayed (mfg_replay) once before returning. */
 int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
              int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
              uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream);
@@ -209,6 +210,13 @@ int mfg_replay(mfg_engine* e, void* stream);
 int mfg_layout(const mfg_engine* e, int32_t* out);
 void* mfg_state_ptr(mfg_engine* e);
 int64_t mfg_state_bytes(const mfg_engine* e);
+/* Per-kernel timing (HIP events recorded around every launch on the launch stream while enabled).
+ * Kernel ids: MFG_K_LOGIC, MFG_K_RESETDONE, MFG_K_OBS, MFG_K_REPLAY, MFG_K_RESET.
+ * mfg_profile_read synchronises on the last event, writes total milliseconds and launch counts per
+ * kernel id (n entries, up to MFG_K_COUNT) and clears the accumulators. */
+enum { MFG_K_LOGIC = 0, MFG_K_RESETDONE = 1, MFG_K_OBS = 2, MFG_K_REPLAY = 3, MFG_K_RESET = 4, MFG_K_COUNT = 5 };
+int mfg_profile(mfg_engine* e, int enable);
+int mfg_profile_read(mfg_engine* e, double* total_ms, int64_t* launches, int n);
 /* Snapshots (checkpoint / resume, parity fixtures): whole state buffer device <-> device. */
 int mfg_export_state(mfg_engine* e, void* dst, void* stream);
 int mfg_import_state(mfg_engine* e, const void* src, void* stream);

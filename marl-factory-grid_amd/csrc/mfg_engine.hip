@@ -1628,7 +1628,26 @@ struct mfg_engine {
   std::vector<void*> d_bufs;
   uint8_t* d_state = nullptr;
   int maxpts = 0;
+  // per-kernel timing (mfg_profile)
+  bool prof = false;
+  std::vector<hipEvent_t> ev_free;
+  struct Mark { int k; hipEvent_t a, b; };
+  std::vector<Mark> marks;
 };
+
+static hipEvent_t prof_event(mfg_engine* e) {
+  if (!e->ev_free.empty()) {
+    hipEvent_t ev = e->ev_free.back();
+    e->ev_free.pop_back();
+    return ev;
+  }
+  hipEvent_t ev = nullptr;
+  if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+  return ev;
+}
+// bracket one launch with events when profiling (PROF_BEGIN before, PROF_END after the launch)
+#define PROF_BEGIN(E, ST) hipEvent_t _pa = nullptr; if ((E)->prof) { _pa = prof_event(E); if (_pa) (void)hipEventRecord(_pa, ST); }
+#define PROF_END(E, ST, KID) if (_pa) { hipEvent_t _pb = prof_event(E); if (_pb) { (void)hipEventRecord(_pb, ST); (E)->marks.push_back({KID, _pa, _pb}); } }
 
 static thread_local std::string g_err;
 static int fail(const std::string& m) {
@@ -1865,6 +1884,8 @@ extern "C" int mfg_destroy(mfg_engine* e) {
   for (void* p : e->d_bufs) (void)hipFree(p);
   if (e->d_spec) (void)hipFree(e->d_spec);
   if (e->d_state) (void)hipFree(e->d_state);
+  for (auto& m : e->marks) { e->ev_free.push_back(m.a); e->ev_free.push_back(m.b); }
+  for (hipEvent_t ev : e->ev_free) (void)hipEventDestroy(ev);
   delete e;
   return 0;
 }
@@ -1904,12 +1925,14 @@ static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
 // render obs of every env into obs (obs_dtype 0 = f32, 1 = f64)
 static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st) {
   hipError_t err = hipSuccess;
+  PROF_BEGIN(e, st);
   if (obs_dtype == 1) {
     DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double>(e, (double*)obs, st)));
   } else {
     DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float>(e, (float*)obs, st)));
   }
   if (err != hipSuccess) return fail(std::string("k_obs launch: ") + hipGetErrorString(err));
+  PROF_END(e, st, MFG_K_OBS);
   return 0;
 }
 
@@ -1919,10 +1942,12 @@ extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_
                          uint64_t seed_base, void* stream) {
   if (!e) return fail("null engine");
   hipStream_t st = (hipStream_t)stream;
+  PROF_BEGIN(e, st);
   hipLaunchKernelGGL(k_reset, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_full * MFG_WPB, st, e->d_spec,
                      e->d_state, (long long)e->B, mask, init, (unsigned long long)seed_base);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_reset launch: ") + hipGetErrorString(err));
+  PROF_END(e, st, MFG_K_RESET);
   return obs ? launch_obs(e, obs, obs_dtype, st) : 0;
 }
 
@@ -1930,10 +1955,13 @@ extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_
 extern "C" int mfg_replay(mfg_engine* e, void* stream) {
   if (!e) return fail("null engine");
   const size_t lds = (size_t)e->h.lds_replay_per_wave * MFG_WPB;
-  hipLaunchKernelGGL(k_replay, dim3(env_grid(e)), dim3(MFG_WPB * 64), lds, (hipStream_t)stream, e->d_spec, e->d_state,
+  hipStream_t st = (hipStream_t)stream;
+  PROF_BEGIN(e, st);
+  hipLaunchKernelGGL(k_replay, dim3(env_grid(e)), dim3(MFG_WPB * 64), lds, st, e->d_spec, e->d_state,
                      (long long)e->B);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
+  PROF_END(e, st, MFG_K_REPLAY);
   return 0;
 }
 
@@ -1953,6 +1981,8 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
   const size_t obs_row = B * A * (size_t)e->h.obs_agent_stride * (obs_dtype == 1 ? 8 : 4);
   for (int k = 0; k < K; k++) {
     const size_t kb = (size_t)k * B;
+    {
+    PROF_BEGIN(e, st);
     hipLaunchKernelGGL(k_logic, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
@@ -1961,11 +1991,15 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
                        auto_reset);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(std::string("k_logic launch: ") + hipGetErrorString(err));
+    PROF_END(e, st, MFG_K_LOGIC);
+    }
     if (auto_reset) {
+      PROF_BEGIN(e, st);
       hipLaunchKernelGGL(k_resetdone, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_full * MFG_WPB, st,
                          e->d_spec, e->d_state, (long long)e->B);
-      err = hipGetLastError();
+      hipError_t err = hipGetLastError();
       if (err != hipSuccess) return fail(std::string("k_resetdone launch: ") + hipGetErrorString(err));
+      PROF_END(e, st, MFG_K_RESETDONE);
     }
 #ifndef MFG_ABLATE_NOOBS
     if (obs && launch_obs(e, (uint8_t*)obs + (size_t)k * obs_row, obs_dtype, st)) return -1;
@@ -1985,5 +2019,26 @@ extern "C" int mfg_import_state(mfg_engine* e, const void* src, void* stream) {
   HIPCHK(hipMemcpyAsync(e->d_state, src, (size_t)e->h.L.size * e->B, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
 }
+extern "C" int mfg_profile(mfg_engine* e, int enable) {
+  if (!e) return fail("null engine");
+  e->prof = enable != 0;
+  return 0;
+}
+
+extern "C" int mfg_profile_read(mfg_engine* e, double* total_ms, int64_t* launches, int n) {
+  if (!e || !total_ms || !launches) return fail("null argument");
+  for (int k = 0; k < n; k++) { total_ms[k] = 0.0; launches[k] = 0; }
+  if (!e->marks.empty()) HIPCHK(hipEventSynchronize(e->marks.back().b));
+  for (const auto& m : e->marks) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, m.a, m.b));
+    if (m.k < n) { total_ms[m.k] += ms; launches[m.k] += 1; }
+    e->ev_free.push_back(m.a);
+    e->ev_free.push_back(m.b);
+  }
+  e->marks.clear();
+  return 0;
+}
+
 extern "C" int64_t mfg_state_bytes(const mfg_engine* e) { return e ? (int64_t)e->h.L.size * e->B : -1; }
 extern "C" int mfg_abi_version(void) { return MFG_ABI_VERSION; }

@@ -14,6 +14,7 @@ from . import abi
 
 LIB_PATH = Path(os.environ.get('MFG_HIP_LIB') or Path(__file__).resolve().parent / '_lib' / 'libmfg_hip.so')
 EV_MISC = 10
+KERNELS = ['k_logic', 'k_resetdone', 'k_obs', 'k_replay', 'k_reset']  # MFG_K_* ids (include/mfg.h)
 
 LAYOUT_KEYS = ['size', 'o_hdr', 'o_rule_ctr', 'o_agent_pos', 'o_agent_arr', 'o_agent_par', 'o_frozen_org',
                'o_frozen_gp', 'o_door', 'o_items', 'o_pods', 'o_drops', 'o_dests', 'o_dirt_pos', 'o_dirt_id',
@@ -57,6 +58,10 @@ def load_lib():
     L.mfg_import_state.restype = C.c_int
     L.mfg_state_bytes.argtypes = [C.c_void_p]
     L.mfg_state_bytes.restype = C.c_int64
+    L.mfg_profile.argtypes = [C.c_void_p, C.c_int]
+    L.mfg_profile.restype = C.c_int
+    L.mfg_profile_read.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    L.mfg_profile_read.restype = C.c_int
     L.mfg_abi_version.restype = C.c_int
     if L.mfg_abi_version() != 1:
         raise RuntimeError('libmfg_hip.so ABI version mismatch')
@@ -125,6 +130,19 @@ class Engine:
         _check(self.L.mfg_step(self.h, int(K), _ptr(actions), int(philox_seed) & 0xFFFFFFFF, int(env_base),
                                int(step_base), _ptr(reward), _ptr(done), _ptr(obs), dt, _ptr(ev_act),
                                _ptr(ev_watch), _ptr(ev_misc), int(bool(auto_reset)), self._stream()), 'mfg_step')
+
+    def profile(self, enable=True):
+        """Record HIP events around every kernel launch (on the launch stream) while enabled."""
+        _check(self.L.mfg_profile(self.h, int(bool(enable))), 'mfg_profile')
+
+    def profile_read(self):
+        """{kernel: (total_ms, launches)} since the last read (synchronises on the last event)."""
+        n = len(KERNELS)
+        ms = np.zeros(n, np.float64)
+        cnt = np.zeros(n, np.int64)
+        _check(self.L.mfg_profile_read(self.h, ms.ctypes.data_as(C.c_void_p), cnt.ctypes.data_as(C.c_void_p), n),
+               'mfg_profile_read')
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(KERNELS)}
 
     def export_state(self):
         t = self.torch.empty((self.B, self.layout['size']), dtype=self.torch.uint8, device=self.device)

@@ -1,0 +1,88 @@
+"""Multi-process (gloo, world_size 2) coverage of the sharded path on CPU: each rank owns a contiguous
+env range keyed by global env index, steps its envs independently (C oracle as the per-env stepper —
+on the GPU box the HIP engine takes this place), and only a metrics vector is all-reduced. The union of
+the ranks' results must equal a single-process run over all envs."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from mfg_amd.shard import env_range, split_global
+
+STEPS, PER_RANK, SEED = 60, 3, 77
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rollout(first, count):
+    import oracle as O
+    from philox import synthetic_actions
+    from mfg_amd.spec import compile_spec
+    spec = compile_spec('rooms4.yaml')
+    out = []
+    for env in range(first, first + count):
+        e = O.OracleEnv(spec, 500 + env)
+        e.reset()
+        rs, eps = [], 0
+        for t in range(STEPS):
+            r, d, _ = e.step(synthetic_actions(SEED, [env], t, spec.n_actions)[0])
+            rs.append(list(r))
+            if d:
+                eps += 1
+                e.reset()
+        out.append((env, np.asarray(rs), eps))
+    return out
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    first, count = env_range(rank, world, PER_RANK)
+    res = _rollout(first, count)
+    from mfg_amd.shard import allreduce_metrics
+    m = allreduce_metrics(torch.tensor([float(sum(r.sum() for _, r, _ in res)), float(len(res) * STEPS)],
+                                       dtype=torch.float64))
+    q.put((rank, [(e, r.tolist(), n) for e, r, n in res], m.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_env_ranges():
+    assert [env_range(r, 4, 10) for r in range(4)] == [(0, 10), (10, 10), (20, 10), (30, 10)]
+    parts = [split_global(r, 3, 10) for r in range(3)]
+    assert parts == [(0, 4), (4, 3), (7, 3)] and sum(c for _, c in parts) == 10
+    with pytest.raises(ValueError):
+        env_range(2, 2, 5)
+
+
+def test_gloo_world2_matches_single_process():
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = {e: (r, n) for e, r, n in _rollout(0, world * PER_RANK)}
+    total = 0.0
+    for rank, res, metrics in got:
+        for e, r, n in res:
+            assert np.array_equal(np.asarray(r), ref[e][0]) and n == ref[e][1], f'env {e} on rank {rank}'
+            total += float(np.asarray(r).sum())
+    for _, _, metrics in got:
+        assert metrics[1] == world * PER_RANK * STEPS
+        assert abs(metrics[0] - total) < 1e-9
