@@ -185,9 +185,13 @@ int mfg_destroy(mfg_engine* e);
 const char* mfg_last_error(void);
 
 /* Reset envs (mask[b] != 0, or all if mask == NULL); Factory.reset (factory.py:134-148).
- * init = 1 additionally creates the envs: env b is seeded like `random.seed(seed_base + b)` before
- * `Factory(cfg)` (SURVEY §8c seeding contract). obs (device, may be NULL): [B][A][lmax][d][d],
- * obs_dtype 0 = float32, 1 = float64. */
+ * init = 0: reset existing envs. init & MFG_INIT_CREATE: first create the envs (Factory.__init__,
+ * factory.py:81-129): env b is seeded like `random.seed(seed_base + b)` before `Factory(cfg)` (SURVEY
+ * §8c seeding contract), or, with MFG_INIT_KEEP_MT, keeps the MT19937 state + index already imported
+ * into its record (mfg_import_state), e.g. the caller's Python `random` state. MFG_INIT_NO_RESET stops
+ * after creation (the reference's constructor does not reset). obs (device, may be NULL):
+ * [B][A][lmax][d][d], obs_dtype 0 = float32, 1 = float64. */
+enum { MFG_INIT_CREATE = 1, MFG_INIT_KEEP_MT = 2, MFG_INIT_NO_RESET = 4 };
 int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init, uint64_t seed_base,
               void* stream);
 

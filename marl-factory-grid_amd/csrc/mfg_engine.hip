@@ -1449,12 +1449,24 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, ui
   Env e;
   env_full(S, smem + (size_t)wid * S->lds_full, e);
   uint8_t* rec = state + (size_t)env * S->L.size;
-  if (init) {
-    for (int i = e.lane; i < (S->L.size >> 2); i += MFG_WAVE) ((int*)e.lds)[i] = 0;
-    wave_sync();
-    const unsigned long long py_seed = seed_base + (unsigned long long)env;
-    uint32_t key[2] = {(uint32_t)py_seed, (uint32_t)(py_seed >> 32)};
-    mt_seed(e, key, key[1] ? 2 : 1);
+  if (init & MFG_INIT_CREATE) {
+    if (init & MFG_INIT_KEEP_MT) {
+      // MT19937 state imported by the caller (e.g. Python's global `random` state): keep it, zero the rest
+      rec_copy(e.lds, rec, S->L.size, e.lane);
+      wave_sync();
+      const int mt_idx = e.H(H_MT_IDX);
+      const int w0 = S->L.o_mt >> 2, w1 = (S->L.o_mt >> 2) + 624;
+      for (int i = e.lane; i < (S->L.size >> 2); i += MFG_WAVE)
+        if (i < w0 || i >= w1) ((int*)e.lds)[i] = 0;
+      wave_sync();
+      e.setH(H_MT_IDX, mt_idx);
+    } else {
+      for (int i = e.lane; i < (S->L.size >> 2); i += MFG_WAVE) ((int*)e.lds)[i] = 0;
+      wave_sync();
+      const unsigned long long py_seed = seed_base + (unsigned long long)env;
+      uint32_t key[2] = {(uint32_t)py_seed, (uint32_t)(py_seed >> 32)};
+      mt_seed(e, key, key[1] ? 2 : 1);
+    }
     for (int i = e.lane; i < S->nf; i += MFG_WAVE) e.perm()[i] = (uint16_t)S->floor_init[i];
     if (e.lane == 0) {
       e.pcg()[0] = S->pcg_init_hi; e.pcg()[1] = S->pcg_init_lo;
@@ -1473,8 +1485,10 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, ui
     rec_copy(e.lds, rec, S->L.size, e.lane);
     wave_sync();
   }
-  env_reset(e, e.scratch);
-  e.setH(H_OBS_INIT, 1);  // the reference renders right after every reset
+  if (!(init & MFG_INIT_NO_RESET)) {
+    env_reset(e, e.scratch);
+    e.setH(H_OBS_INIT, 1);  // the reference renders right after every reset
+  }
   e.setH(H_DONE, 0);
   wave_sync();
   rec_copy(rec, e.lds, S->L.size, e.lane);
