@@ -90,5 +90,5 @@ struct MfgDevSpec {
   int32_t lds_obs;           // k_obs: lean record + cell map + id-collision pairs
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)
   int32_t lds_replay_per_wave;  // k_replay slice: [hdr 128 B][MT 2496 B][perm as u32][shuffle tables]
-  int32_t replay_perm_off, replay_stab_off, replay_stab_n;
+  int32_t replay_perm_off, replay_sink_off, replay_stab_off, replay_stab_n;
 };

@@ -28,6 +28,10 @@ __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 __device__ __forceinline__ u64 ballot(bool p) { return (u64)__ballot(p); }
 __device__ __forceinline__ int popc(u64 m) { return __popcll(m); }
 __device__ __forceinline__ u64 lt_mask() { return (1ull << lane_id()) - 1ull; }
+// mbcnt(m) in two VALU ops
+__device__ __forceinline__ int mbcnt(u64 m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -115,8 +119,10 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
 __device__ void mt_twist(const Env& e) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
+  // lanes outside a phase store into their own scratch word instead of branching (no exec-mask
+  // juggling); every kernel that owns MT state has a scratch area
+  uint32_t* sink = (uint32_t*)e.scratch + lane;
   uint32_t v[4];
-  // loads are unconditional (clamped indices) so each phase is one batch of LDS reads and one wait
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int i = min(t * MFG_WAVE + lane, 226);
@@ -125,8 +131,9 @@ __device__ void mt_twist(const Env& e) {
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int i = t * MFG_WAVE + lane;
-    if (i < 227) mt[i] = v[t];
+    *(i < 227 ? &mt[i] : sink) = v[t];
   }
+  wave_sync();
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int i = min(227 + t * MFG_WAVE + lane, 453);
@@ -135,8 +142,9 @@ __device__ void mt_twist(const Env& e) {
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int i = 227 + t * MFG_WAVE + lane;
-    if (i < 454) mt[i] = v[t];
+    *(i < 454 ? &mt[i] : sink) = v[t];
   }
+  wave_sync();
 #pragma unroll
   for (int t = 0; t < 3; t++) {
     const int i = min(454 + t * MFG_WAVE + lane, 622);
@@ -145,10 +153,11 @@ __device__ void mt_twist(const Env& e) {
 #pragma unroll
   for (int t = 0; t < 3; t++) {
     const int i = 454 + t * MFG_WAVE + lane;
-    if (i < 623) mt[i] = v[t];
+    *(i < 623 ? &mt[i] : sink) = v[t];
   }
   wave_sync();
-  if (lane == 0) mt[623] = mt_mix(mt[623], mt[0], mt[396]);
+  const uint32_t last = mt_mix(mt[623], mt[0], mt[396]);
+  *(lane == 0 ? &mt[623] : sink) = last;
   wave_sync();
 }
 
@@ -187,28 +196,55 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
   uint32_t ctr = perm ? (uint32_t)uni((int)e.stab[MFG_STAB_CTR]) : 0u;
   while (icur >= lo) {
     if (idx >= 624) {
+#ifndef MFG_ABLATE_NOTWIST
       mt_twist(e);
+#endif
       idx = 0;
     }
     const int lmax = 624 - idx;
     const bool has = lane < lmax;
     const uint32_t y = mt_temper(mt[has ? idx + lane : 623]);
-    int A = lane;
+    int A;
     u64 accm;
     int il;
     uint32_t r;
     bool act, acc;
-    for (;;) {
+    if (icur - 63 >= lo && 32 - __clz(icur + 1) == 32 - __clz(icur - 62)) {
+      // fast path: every lane's i is >= lo and bitlen(i+1) is the same for the whole chunk, so
+      // r_l = y_l >> (32 - k) is fixed and accept_l <=> A_l <= c_l = icur - r_l
+      r = y >> __clz(icur + 1);
+      const int c = has ? icur - (int)r : -1;
+      A = mbcnt(ballot(c >= 63));  // lower bound: the lanes that accept whatever precedes them
+#ifdef MFG_ABLATE_NOJACOBI
+      A = mbcnt(ballot(c >= 0));
+      if (0)
+#endif
+      for (;;) {
+        accm = ballot(A <= c);
+        const int An = mbcnt(accm);
+        if (!ballot(An != A)) break;
+        A = An;
+      }
       il = icur - A;
-      act = has && il >= lo;
-      uint32_t n = act ? (uint32_t)(il + 1) : 2u;
-      int k = 32 - __clz((int)n);
-      r = act ? (y >> (32 - k)) : 0u;
-      acc = act && r <= (uint32_t)il;
+      acc = A <= c;
+      act = has;
+#ifdef MFG_ABLATE_NOJACOBI
       accm = ballot(acc);
-      int An = popc(accm & lt_mask());
-      if (!ballot(An != A)) break;
-      A = An;
+#endif
+    } else {
+      A = lane;
+      for (;;) {
+        il = icur - A;
+        act = has && il >= lo;
+        uint32_t n = act ? (uint32_t)(il + 1) : 2u;
+        int k = 32 - __clz((int)n);
+        r = act ? (y >> (32 - k)) : 0u;
+        acc = act && r <= (uint32_t)il;
+        accm = ballot(acc);
+        int An = mbcnt(accm);
+        if (!ballot(An != A)) break;
+        A = An;
+      }
     }
     const int consumed = popc(ballot(act));
     const int nacc = popc(accm);
@@ -217,8 +253,7 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
     if (perm && nacc) {
       const int i = acc ? il : icur, j = acc ? (int)r : icur;
       const int P0i = perm[i];
-      ctr = (ctr + 1u) & 0x3FFFFFFu;
-      if (ctr == 0u) ctr = 1u;  // never reuse the zero tag of a freshly cleared table
+      ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
       const uint32_t tag = ctr << 6;
       const int imin = icur - nacc + 1;
       if (acc && j >= imin && j != i) atomicMax(&ptab[icur - j], tag | (uint32_t)lane);
@@ -279,6 +314,96 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
   e.setH(H_MT_IDX, idx);
   wave_sync();
   return first_j;
+}
+
+// k_replay's shuffle: the exchange path of mt_randbelow_seq specialised for the replay kernel (64
+// draws per chunk, 32-bit perm). Out-of-play lanes read and write a per-lane sink word instead of
+// branching, so a block runs without exec-mask changes. stab: [64] rank table (tag << 6 | lane),
+// [64] chunk counter.
+#define RP_CTR 64
+#define RP_STAB_N 68
+__device__ void replay_shuffle(const Env& e, uint32_t* perm) {
+  uint32_t* mt = e.mt();
+  const int lane = e.lane;
+  uint32_t* sink = (uint32_t*)e.scratch + lane;
+  uint32_t* ptab = e.stab;
+  const int lo = 1;
+  int idx = e.H(H_MT_IDX);
+  int icur = e.S->nf - 1;
+  uint32_t ctr = (uint32_t)uni((int)e.stab[RP_CTR]);
+  while (icur >= lo) {
+    if (idx >= 624) {
+#ifndef MFG_ABLATE_NOTWIST
+      mt_twist(e);
+#endif
+      idx = 0;
+    }
+    const bool has = lane < 624 - idx;
+    const uint32_t y = mt_temper(mt[has ? idx + lane : 623]);
+    int A;
+    uint32_t r;
+    bool act, acc;
+    u64 m;
+    if (icur - 63 >= lo && __clz(icur + 1) == __clz(icur - 62)) {
+      // fast path: i >= lo and bitlen(i+1) constant over the chunk -> accept <=> A <= c = icur - r
+      r = y >> __clz(icur + 1);
+      const int c = has ? icur - (int)r : -1;
+      A = mbcnt(ballot(c >= 63));
+      for (;;) {
+        m = ballot(A <= c);
+        const int n = mbcnt(m);
+        if (!ballot(n != A)) break;
+        A = n;
+      }
+      acc = A <= c;
+      act = has;
+    } else {
+      A = lane;
+      for (;;) {
+        const int il = icur - A;
+        act = has && il >= lo;
+        r = act ? y >> __clz(il + 1) : 0u;
+        acc = act && r <= (uint32_t)il;
+        m = ballot(acc);
+        const int n = mbcnt(m);
+        if (!ballot(n != A)) break;
+        A = n;
+      }
+    }
+    const int consumed = popc(ballot(act));
+    const int nacc = popc(m);
+#ifndef MFG_ABLATE_NOSWAP
+    if (nacc) {
+      const int imin = icur - nacc + 1;
+      const int i = icur - A, j = (int)r;
+      uint32_t* pi = acc ? &perm[i] : sink;
+      const int P0 = (int)*pi;
+      ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
+      const uint32_t tag = ctr << 6;
+      // pi: last earlier draw whose j is this draw's i (rank table keyed by icur - j; self-swaps excluded)
+      atomicMax(acc && j >= imin && j != i ? &ptab[icur - j] : sink, tag | (uint32_t)lane);
+      wave_sync();
+      const uint32_t tp = ptab[A & 63];
+      int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
+      int v = P0;
+      while (ballot(ptr >= 0)) {
+        const int src = ptr >= 0 ? ptr : lane;
+        const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
+        if (ptr >= 0) { v = v2; ptr = p2; }
+      }
+      // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j]
+      const uint32_t F = atomicExch(acc ? &perm[j] : sink, (uint32_t)v);
+      wave_sync();
+      *pi = F;
+      wave_sync();
+    }
+#endif
+    icur -= nacc;
+    idx += consumed;
+  }
+  if (lane == 0) e.stab[RP_CTR] = ctr;
+  e.setH(H_MT_IDX, idx);
+  wave_sync();
 }
 
 // random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
@@ -500,7 +625,7 @@ __device__ int free_positions(const Env& e, int n, int* out) {
     int cell = i < nf ? (int)perm[i] : -1;
     bool f = i < nf && lane_cell_free(e, cell);
     u64 m = ballot(f);
-    int rank = k + popc(m & lt_mask());
+    int rank = k + mbcnt(m);
     if (f && rank < n) out[rank] = cell;
     k += popc(m);
   }
@@ -753,6 +878,7 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
 // ------------------------------------------------------------------------------------------------
 // rules (environment/rules.py, modules/*/rules.py); hook order states.py:170-226
 // ------------------------------------------------------------------------------------------------
+template <bool RNG>
 __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
   SpecP S = e.S;
   const CS mfg_rule& ru = S->s.rules[ri];
@@ -802,8 +928,9 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
     int c = uni(e.rctr()[ri]);
     if (c < 0) {
     } else if (!c) {
-      int valid;
-      int v = dirt_trigger_spawn(e, ru.i[1], ru.f[0], &valid, scratch);
+      int valid = 0, v = 0;
+      if constexpr (RNG) v = dirt_trigger_spawn(e, ru.i[1], ru.f[0], &valid, scratch);
+      else o.crashed = 1;  // unreachable: the host stages the full record for specs with RespawnDirt
       o.dirt_spawn_value = v;
       o.dirt_spawn_valid = valid;
       wave_sync();
@@ -958,7 +1085,7 @@ __device__ void env_reset(const Env& e, int* scratch) {
       const int i = b + e.lane;
       const bool em = i < nf && lane_cell_empty(e, perm[i < nf ? i : 0]);
       const u64 mm = ballot(em);
-      const int rank = k + popc(mm & lt_mask());
+      const int rank = k + mbcnt(mm);
       const u64 hitm = ballot(em && rank == j);
       if (hitm) cell = rl(i < nf ? (int)perm[i] : 0, ffs64(hitm));
       k += popc(mm);
@@ -1073,20 +1200,6 @@ struct RayVis {
   const RayLane* rl_;
 };
 
-// rank of the first visit of `cell` (ray index * 32 + point index), or 1<<30 if not visible
-template <int MAXPTS>
-__device__ int first_visit(const RayVis& rv, int cell) {
-  int k = -1;
-  const int cx = cell / rv.W, cy = cell % rv.W;
-#pragma unroll
-  for (int p = 0; p < MAXPTS; p++)
-    if (k < 0 && ((rv.vism >> p) & 1u) && rv.ox + rv.rl_->dx(p) == cx && rv.oy + rv.rl_->dy(p) == cy) k = p;
-  const u64 m = ballot(k >= 0);
-  if (!m) return 1 << 30;
-  const int L = ffs64(m);
-  return L * 32 + rl(k, L);
-}
-
 // Identifier-collision candidates (Q14), agent independent, built once per render into scratch:
 // pair q = {cellA, cellB, codeA, codeB}; code = kind << 8 | slot (kind: 1 door, 3 item, 4 pod, 5 drop,
 // 6 dirt, 7 dest, 9 wall -> slot unused, the wall is identified by its cell). Returns the pair count.
@@ -1115,7 +1228,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const bool has = id >= 0 && id < S->nw;
     const int wc = has ? S->wall_cells[id] : 0;
     const u64 m = ballot(has);
-    const int rank = n + popc(m & lt_mask());
+    const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
       pairs[4 * rank] = cell; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = 9 << 8;
     }
@@ -1126,7 +1239,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const bool has = id >= 0 && id < S->nd && (e.door()[id < S->nd && id >= 0 ? id : 0] & DW_PRESENT);
     const int dc = has ? S->door_cells[id] : 0;
     const u64 m = ballot(has);
-    const int rank = n + popc(m & lt_mask());
+    const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
       pairs[4 * rank] = cell; pairs[4 * rank + 1] = dc; pairs[4 * rank + 2] = code;
       pairs[4 * rank + 3] = (K_DOOR << 8) | id;
@@ -1138,7 +1251,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const int idj = rl(id, j), kj = rl(kind, j), cj = rl(cell, j), codej = rl(code, j);
     const bool has = lane < j && id >= 0 && idj == id && kj != kind;
     const u64 m = ballot(has);
-    const int rank = n + popc(m & lt_mask());
+    const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
       pairs[4 * rank] = cell; pairs[4 * rank + 1] = cj; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = codej;
     }
@@ -1154,7 +1267,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
       has = (e.door()[k] & DW_PRESENT) != 0;
     }
     const u64 m = ballot(has);
-    const int rank = n + popc(m & lt_mask());
+    const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
       pairs[4 * rank] = dc; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = (K_DOOR << 8) | k;
       pairs[4 * rank + 3] = 9 << 8;
@@ -1171,7 +1284,7 @@ struct Sup {  // per-agent suppression sets from the identifier dedupe
   u64 walls;  // window cells whose wall is suppressed (walls outside the window are never placed)
   int ax, ay, r, d, W;
 };
-__device__ __forceinline__ void sup_add(Sup& s, int code, int cell) {
+__device__ __forceinline__ void sup_add(Sup& s, int code, int xy) {
   const int kind = code >> 8, slot = code & 0xFF;
   const u64 bit = 1ull << (slot & 63);
   switch (kind) {
@@ -1182,7 +1295,7 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int cell) {
     case K_DIRT: s.dirt |= bit; break;
     case K_DOOR: s.doors |= bit; break;
     default: {
-      const int px = cell / s.W - s.ax + s.r, py = cell % s.W - s.ay + s.r;
+      const int px = (xy >> 16) - s.ax + s.r, py = (xy & 0xFFFF) - s.ay + s.r;
       if (px >= 0 && py >= 0 && px < s.d && py < s.d) s.walls |= 1ull << (px * s.d + py);
       break;
     }
@@ -1198,13 +1311,23 @@ __device__ void build_obs(const Env& e, OT* out_env) {
   build_cmap(e);
   int* pairs = e.scratch;
   const int npairs = build_id_pairs(e, pairs);
+  for (int q = lane; q < npairs; q += MFG_WAVE) {  // cells -> packed (x << 16 | y), agent independent
+    const int cA = pairs[4 * q], cB = pairs[4 * q + 1];
+    pairs[4 * q] = ((cA / W) << 16) | (cA % W);
+    pairs[4 * q + 1] = ((cB / W) << 16) | (cB % W);
+  }
+  wave_sync();
+  // first-visit table of the dedupe: (2d+1)^2 cells around the ray origin, rank = ray * 32 + point
+  uint32_t* fv = (uint32_t*)(e.scratch + 4 * OBS_MAX_PAIRS);
+  const int fw = 2 * d + 1, fn = fw * fw;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
   const int agp = lane < A ? e.agpos()[lane] : -1;
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
   const int nT = e.H(H_N_DIRT);
   // this lane's ray, loaded once: 16 packed bytes
-  RayLane ray;
+  RayLane ray0;
   {
+    RayLane& ray = ray0;
     const bool has = lane < S->nrays;
     const int8_t* pts = S->ray_pts + (size_t)(has ? lane : 0) * MAXPTS * 2;
 #pragma unroll
@@ -1220,6 +1343,10 @@ __device__ void build_obs(const Env& e, OT* out_env) {
   const bool inwin = lane < dd;
   const int wpx = lane / d, wpy = lane % d;
   for (int a = 0; a < A; a++) {
+    // opaque copy: keeps the compiler from hoisting every per-point offset, address and rank out of
+    // the agent loop (that trades ~40 VGPRs and half the occupancy for a few bit-field extracts)
+    RayLane ray = ray0;
+    asm volatile("" : "+v"(ray.pk[0]), "+v"(ray.pk[1]), "+v"(ray.pk[2]), "+v"(ray.pk[3]));
     const int apos = rl(agp, a);
     const int ax = apos / W, ay = apos % W;
     const int org = rl(org_l, a);
@@ -1255,21 +1382,32 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     Sup sup;
     sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = sup.walls = 0;
     sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
+    bool fv_built = false;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
-      const int cA = q < npairs ? pairs[4 * q] : 0, cB = q < npairs ? pairs[4 * q + 1] : 0;
-      const bool nearq = q < npairs && abs(cA / W - ox) <= d && abs(cA % W - oy) <= d && abs(cB / W - ox) <= d &&
-                         abs(cB % W - oy) <= d;
-      u64 m = ballot(nearq);
-      while (m) {
-        const int L = ffs64(m);
-        m &= m - 1;
-        const int ca = rl(cA, L), cb = rl(cB, L);
-        const int rA = first_visit<MAXPTS>(rv, ca), rB = first_visit<MAXPTS>(rv, cb);
-        if (rA >= (1 << 30) || rB >= (1 << 30)) continue;
+      const int pA = q < npairs ? pairs[4 * q] : 0, pB = q < npairs ? pairs[4 * q + 1] : 0;
+      const int xA = (pA >> 16) - ox + d, yA = (pA & 0xFFFF) - oy + d;
+      const int xB = (pB >> 16) - ox + d, yB = (pB & 0xFFFF) - oy + d;
+      const bool nearq = q < npairs && (unsigned)xA < (unsigned)fw && (unsigned)yA < (unsigned)fw &&
+                         (unsigned)xB < (unsigned)fw && (unsigned)yB < (unsigned)fw;
+      if (!ballot(nearq)) continue;
+      if (!fv_built) {  // min rank over (ray, point) of every visible point, in origin-local coordinates
+        fv_built = true;
+        for (int i = lane; i < fn; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
+        wave_sync();
+#pragma unroll
+        for (int p = 0; p < MAXPTS; p++)
+          if ((rv.vism >> p) & 1u) atomicMin(&fv[(ray.dx(p) + d) * fw + ray.dy(p) + d], (uint32_t)(lane * 32 + p));
+        wave_sync();
+      }
+      const uint32_t rA = nearq ? fv[xA * fw + yA] : 0xFFFFFFFFu, rB = nearq ? fv[xB * fw + yB] : 0xFFFFFFFFu;
+      u64 hm = ballot(rA != 0xFFFFFFFFu && rB != 0xFFFFFFFFu);
+      while (hm) {
+        const int L = ffs64(hm);
+        hm &= hm - 1;
         const int qq = q0 + L;
-        if (rA < rB) sup_add(sup, pairs[4 * qq + 3], cb);
-        else sup_add(sup, pairs[4 * qq + 2], ca);
+        if (rl((int)rA, L) < rl((int)rB, L)) sup_add(sup, pairs[4 * qq + 3], rl(pB, L));
+        else sup_add(sup, pairs[4 * qq + 2], rl(pA, L));
       }
     }
     // ---- placement (lane = window cell): tag bits from the cell map, values composed per layer ----
@@ -1351,6 +1489,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
 // ------------------------------------------------------------------------------------------------
 #define MFG_EV_MISC 10
 
+template <bool RNG>
 __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   SpecP S = e.S;
   const int A = S->A;
@@ -1367,7 +1506,7 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   }
   const int nr = S->s.n_rules;
   if (!o.crashed)
-    for (int r = 0; r < nr && !o.crashed; r++) rule_tick_step(e, o, r, scratch);
+    for (int r = 0; r < nr && !o.crashed; r++) rule_tick_step<RNG>(e, o, r, scratch);
   if (!o.crashed)
     for (int r = 0; r < nr && !o.crashed; r++) rule_post_step(e, o, r);
   if (!o.crashed)
@@ -1494,7 +1633,9 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, ui
   rec_copy(rec, e.lds, S->L.size, e.lane);
 }
 
-// One env-step of every env (no reset, no render).
+// One env-step of every env (no reset, no render). FULL: the spec consumes the floor order inside a
+// step (S->step_rng), so the whole record incl. MT/perm is staged; otherwise only the lean prefix.
+template <bool FULL>
 __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, uint8_t* state, long long B,
                                                         const int32_t* actions, unsigned philox_seed,
                                                         unsigned env_base, long long step, double* reward,
@@ -1507,7 +1648,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
   if (env >= B) return;
   Env e;
   uint8_t* slice = smem + (size_t)wid * S->lds_logic;
-  const bool full = S->step_rng != 0;
+  constexpr bool full = FULL;
   if (full) {
     env_full(S, slice, e);
   } else {
@@ -1529,7 +1670,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
     }
   }
   StepOut o;
-  env_step(e, my_act, o, e.scratch);
+  env_step<FULL>(e, my_act, o, e.scratch);
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
   if (o.done && auto_reset) e.setH(H_DONE, 1);
   wave_sync();
@@ -1595,7 +1736,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   e.S = S;
   e.lds = smem + (size_t)wid * S->lds_replay_per_wave - S->L.o_mt + 4 * MFG_HDR_N;
   e.lane = lane_id();
-  e.scratch = nullptr;
+  e.scratch = (int*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_sink_off);
   e.cmap = nullptr;
   e.stab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_stab_off);
   e.hdrp = (int*)(smem + (size_t)wid * S->lds_replay_per_wave);
@@ -1617,7 +1758,16 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   }
   for (int i = e.lane; i < S->replay_stab_n; i += MFG_WAVE) e.stab[i] = 0u;
   wave_sync();
-  pay_debt_t(e, p32);
+  if (S->xchg_ordered) {
+#ifndef MFG_ABLATE_NODEBT
+    const int debt = e.H(H_DEBT);
+    for (int k = 0; k < debt; k++) replay_shuffle(e, p32);
+#endif
+    e.setH(H_DEBT, 0);
+    wave_sync();
+  } else {
+    pay_debt_t(e, p32);
+  }
   {
     const uint4* src = (const uint4*)(e.lds + S->L.o_mt);
     uint4* dst = (uint4*)(rec + S->L.o_mt);
@@ -1832,13 +1982,14 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   h.map_bytes = align_up(HW, 16);
   h.lds_full = align_up(h.L.size + 2048 + 4 * MFG_STAB_N, 16);
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
-  h.lds_obs = align_up(h.L.o_mt, 16) + h.map_bytes + 16 * OBS_MAX_PAIRS;
+  h.lds_obs = align_up(h.L.o_mt, 16) + h.map_bytes + 16 * OBS_MAX_PAIRS + align_up(4 * (2 * h.d + 1) * (2 * h.d + 1), 16);
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
     h.replay_perm_off = 4 * MFG_HDR_N + 4 * 624;
-    h.replay_stab_off = h.replay_perm_off + align_up(4 * (h.nf + 1), 16);
-    h.replay_stab_n = h.xchg_ordered ? MFG_STAB_PTAB : MFG_STAB_N;
+    h.replay_sink_off = h.replay_perm_off + align_up(4 * (h.nf + 1), 16);
+    h.replay_stab_off = h.replay_sink_off + 4 * MFG_WAVE;
+    h.replay_stab_n = h.xchg_ordered ? RP_STAB_N : MFG_STAB_N;
     h.lds_replay_per_wave = align_up(h.replay_stab_off + 4 * h.replay_stab_n, 16);
   }
   pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
@@ -1997,12 +2148,21 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
     const size_t kb = (size_t)k * B;
     {
     PROF_BEGIN(e, st);
-    hipLaunchKernelGGL(k_logic, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+    if (e->h.step_rng) {
+    hipLaunchKernelGGL(k_logic<true>, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
                        auto_reset);
+    } else {
+    hipLaunchKernelGGL(k_logic<false>, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
+                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
+                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
+                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
+                       auto_reset);
+    }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(std::string("k_logic launch: ") + hipGetErrorString(err));
     PROF_END(e, st, MFG_K_LOGIC);
