@@ -87,7 +87,8 @@ struct MfgDevSpec {
   MfgLayout L;
   int32_t lds_full;          // bytes of dynamic LDS per wave: full record + scratch + shuffle tables
   int32_t lds_logic;         // k_logic: lean record (o_mt bytes) or lds_full when step_rng
-  int32_t lds_obs;           // k_obs: lean record + cell map + id-collision pairs
+  int32_t lds_obs;           // k_obs: lean record + cell map + id-collision pairs + first-visit table + wall sup
+  int32_t fv_words;          // first-visit table entries ((2d+1)^2, rounded up to 4)
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)
   int32_t lds_replay_per_wave;  // k_replay slice: [hdr 128 B][MT 2496 B][perm as u32][shuffle tables]
   int32_t replay_perm_off, replay_sink_off, replay_stab_off, replay_stab_n;

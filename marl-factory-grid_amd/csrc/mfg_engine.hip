@@ -1151,6 +1151,7 @@ __device__ void env_reset(const Env& e, int* scratch) {
 #define CM_DEST 64u    // destination present and not reached
 #define CM_DIRT 128u
 
+__device__ __forceinline__ int v_clamp(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
 __device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
   SpecP S = e.S;
   if (x < 0 || y < 0 || x >= S->s.H || y >= S->s.W) return false;
@@ -1184,20 +1185,27 @@ __device__ void build_cmap(const Env& e) {
   wave_sync();
 }
 
-// One ray per lane: packed (dx, dy) int8 offsets of up to 16 points and the ray length.
+// One ray per lane: packed (dx, dy) int8 offsets of up to MAXPTS points and the ray length.
+template <int MAXPTS>
 struct RayLane {
-  uint32_t pk[4];  // byte 2p = dx of point p, byte 2p+1 = dy (sign-extended on use)
+  static constexpr int NW = (2 * MAXPTS + 3) / 4;
+  uint32_t pk[NW];  // byte 2p = dx of point p, byte 2p+1 = dy (sign-extended on use)
   int len;
   __device__ __forceinline__ int dx(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16)) & 0xFF); }
   __device__ __forceinline__ int dy(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16 + 8)) & 0xFF); }
-};
-
-// Visible points of this lane's ray for one origin: bit p set = point p added entities (not diagonal-cut,
-// in the grid, before the walk stopped).
-struct RayVis {
-  uint32_t vism;
-  int ox, oy, W;
-  const RayLane* rl_;
+  __device__ __forceinline__ void load(SpecP S, int ray) {
+    const bool has = ray < S->nrays;
+    const uint8_t* pts = (const uint8_t*)S->ray_pts + (size_t)(has ? ray : 0) * MAXPTS * 2;
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (4 * q + b < 2 * MAXPTS) w |= (uint32_t)pts[4 * q + b] << (8 * b);
+      pk[q] = w;
+    }
+    len = has ? S->ray_len[ray] : 0;
+  }
 };
 
 // Identifier-collision candidates (Q14), agent independent, built once per render into scratch:
@@ -1281,10 +1289,10 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
 
 struct Sup {  // per-agent suppression sets from the identifier dedupe
   u64 items, pods, drops, dests, dirt, doors;
-  u64 walls;  // window cells whose wall is suppressed (walls outside the window are never placed)
+  uint8_t* wsup;  // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
   int ax, ay, r, d, W;
 };
-__device__ __forceinline__ void sup_add(Sup& s, int code, int xy) {
+__device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
   const int kind = code >> 8, slot = code & 0xFF;
   const u64 bit = 1ull << (slot & 63);
   switch (kind) {
@@ -1296,7 +1304,7 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy) {
     case K_DOOR: s.doors |= bit; break;
     default: {
       const int px = (xy >> 16) - s.ax + s.r, py = (xy & 0xFFFF) - s.ay + s.r;
-      if (px >= 0 && py >= 0 && px < s.d && py < s.d) s.walls |= 1ull << (px * s.d + py);
+      if (px >= 0 && py >= 0 && px < s.d && py < s.d && lane == 0) s.wsup[px * s.d + py] = 1;
       break;
     }
   }
@@ -1316,73 +1324,59 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     pairs[4 * q] = ((cA / W) << 16) | (cA % W);
     pairs[4 * q + 1] = ((cB / W) << 16) | (cB % W);
   }
-  wave_sync();
-  // first-visit table of the dedupe: (2d+1)^2 cells around the ray origin, rank = ray * 32 + point
+  // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
+  // ray * 32 + point; it gives both the window visibility and the dedupe order (Q14)
   uint32_t* fv = (uint32_t*)(e.scratch + 4 * OBS_MAX_PAIRS);
   const int fw = 2 * d + 1, fn = fw * fw;
+  uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
+  const int nsup4 = (dd + 3) >> 2;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
   const int agp = lane < A ? e.agpos()[lane] : -1;
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
   const int nT = e.H(H_N_DIRT);
-  // this lane's ray, loaded once: 16 packed bytes
-  RayLane ray0;
-  {
-    RayLane& ray = ray0;
-    const bool has = lane < S->nrays;
-    const int8_t* pts = S->ray_pts + (size_t)(has ? lane : 0) * MAXPTS * 2;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-        if (4 * q + b < 2 * MAXPTS) w |= (uint32_t)(uint8_t)pts[4 * q + b] << (8 * b);
-      ray.pk[q] = w;
-    }
-    ray.len = has ? S->ray_len[lane] : 0;
-  }
-  const bool inwin = lane < dd;
-  const int wpx = lane / d, wpy = lane % d;
+  const int npass = (S->nrays + MFG_WAVE - 1) / MFG_WAVE;
   for (int a = 0; a < A; a++) {
-    // opaque copy: keeps the compiler from hoisting every per-point offset, address and rank out of
-    // the agent loop (that trades ~40 VGPRs and half the occupancy for a few bit-field extracts)
-    RayLane ray = ray0;
-    asm volatile("" : "+v"(ray.pk[0]), "+v"(ray.pk[1]), "+v"(ray.pk[2]), "+v"(ray.pk[3]));
     const int apos = rl(agp, a);
     const int ax = apos / W, ay = apos % W;
     const int org = rl(org_l, a);
     const int ox = org / W, oy = org % W;
-    // ---- ray walk (lane = ray): blocking bits of all points first, then the walk on bitmasks ----
-    uint32_t blkm = 0, cutm = 0, ing = 0;
+    for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
+    for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
+    wave_sync();
+    // ---- ray walk (lane = ray, 64 rays per pass): blocking bits first, then the walk on bitmasks ----
+    for (int pass = 0; pass < npass; pass++) {
+      const int ray_id = pass * MFG_WAVE + lane;
+      RayLane<MAXPTS> ray;
+      ray.load(S, ray_id);
+      uint32_t blkm = 0, cutm = 0, ing = 0;
 #pragma unroll
-    for (int p = 0; p < MAXPTS; p++) {
-      const int x = ox + ray.dx(p), y = oy + ray.dy(p);
-      ing |= (x >= 0 && y >= 0 && x < H && y < W) ? (1u << p) : 0u;
-      blkm |= light_block(e, x, y) ? (1u << p) : 0u;
-      if (p > 0 && ray.dx(p) != ray.dx(p - 1) && ray.dy(p) != ray.dy(p - 1)) {
-        // diagonal step: cut when both orthogonal neighbours block light (ray_caster.py:89-96)
-        const bool c = light_block(e, x, oy + ray.dy(p - 1)) && light_block(e, ox + ray.dx(p - 1), y);
-        cutm |= c ? (1u << p) : 0u;
+      for (int p = 0; p < MAXPTS; p++) {
+        const int x = ox + ray.dx(p), y = oy + ray.dy(p);
+        ing |= (x >= 0 && y >= 0 && x < H && y < W) ? (1u << p) : 0u;
+        blkm |= light_block(e, x, y) ? (1u << p) : 0u;
+        if (p > 0 && ray.dx(p) != ray.dx(p - 1) && ray.dy(p) != ray.dy(p - 1)) {
+          // diagonal step: cut when both orthogonal neighbours block light (ray_caster.py:89-96)
+          const bool c = light_block(e, x, oy + ray.dy(p - 1)) && light_block(e, ox + ray.dx(p - 1), y);
+          cutm |= c ? (1u << p) : 0u;
+        }
       }
-    }
-    // points walked: up to and including the first blocking/cut point, within the ray length
-    const uint32_t lenm = ray.len >= 32 ? 0xFFFFFFFFu : ((1u << ray.len) - 1u);
-    const uint32_t stopm = (blkm | cutm) & lenm;
-    const uint32_t walked = stopm ? (((stopm & (0u - stopm)) << 1) - 1u) & lenm : lenm;
-    RayVis rv;
-    rv.vism = walked & ~cutm & ing;
-    rv.ox = ox; rv.oy = oy; rv.W = W; rv.rl_ = &ray;
-    u64 wmask = 0;
+      // points walked: up to and including the first blocking/cut point, within the ray length
+      const uint32_t lenm = ray.len >= 32 ? 0xFFFFFFFFu : ((1u << ray.len) - 1u);
+      const uint32_t stopm = (blkm | cutm) & lenm;
+      const uint32_t walked = stopm ? (((stopm & (0u - stopm)) << 1) - 1u) & lenm : lenm;
+      const uint32_t vism = walked & ~cutm & ing;
+      uint32_t* sink = (uint32_t*)(wsup + ((dd + 15) & ~15)) + lane;
 #pragma unroll
-    for (int p = 0; p < MAXPTS; p++) {
-      const int px = ox + ray.dx(p) - ax + r, py = oy + ray.dy(p) - ay + r;
-      if (((rv.vism >> p) & 1u) && px >= 0 && py >= 0 && px < d && py < d) wmask |= 1ull << (px * d + py);
+      for (int p = 0; p < MAXPTS; p++)
+        atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + d) * fw + ray.dy(p) + d] : sink,
+                  (uint32_t)(ray_id * 32 + p));
     }
-    const u64 vis = wave_or64(wmask);
+    wave_sync();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     Sup sup;
-    sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = sup.walls = 0;
+    sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = 0;
     sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
-    bool fv_built = false;
+    sup.wsup = wsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
       const int pA = q < npairs ? pairs[4 * q] : 0, pB = q < npairs ? pairs[4 * q + 1] : 0;
@@ -1390,96 +1384,93 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       const int xB = (pB >> 16) - ox + d, yB = (pB & 0xFFFF) - oy + d;
       const bool nearq = q < npairs && (unsigned)xA < (unsigned)fw && (unsigned)yA < (unsigned)fw &&
                          (unsigned)xB < (unsigned)fw && (unsigned)yB < (unsigned)fw;
-      if (!ballot(nearq)) continue;
-      if (!fv_built) {  // min rank over (ray, point) of every visible point, in origin-local coordinates
-        fv_built = true;
-        for (int i = lane; i < fn; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
-        wave_sync();
-#pragma unroll
-        for (int p = 0; p < MAXPTS; p++)
-          if ((rv.vism >> p) & 1u) atomicMin(&fv[(ray.dx(p) + d) * fw + ray.dy(p) + d], (uint32_t)(lane * 32 + p));
-        wave_sync();
-      }
       const uint32_t rA = nearq ? fv[xA * fw + yA] : 0xFFFFFFFFu, rB = nearq ? fv[xB * fw + yB] : 0xFFFFFFFFu;
       u64 hm = ballot(rA != 0xFFFFFFFFu && rB != 0xFFFFFFFFu);
       while (hm) {
         const int L = ffs64(hm);
         hm &= hm - 1;
         const int qq = q0 + L;
-        if (rl((int)rA, L) < rl((int)rB, L)) sup_add(sup, pairs[4 * qq + 3], rl(pB, L));
-        else sup_add(sup, pairs[4 * qq + 2], rl(pA, L));
+        if (rl((int)rA, L) < rl((int)rB, L)) sup_add(sup, pairs[4 * qq + 3], rl(pB, L), lane);
+        else sup_add(sup, pairs[4 * qq + 2], rl(pA, L), lane);
       }
     }
-    // ---- placement (lane = window cell): tag bits from the cell map, values composed per layer ----
-    const int x = ax - r + wpx, y = ay - r + wpy;
-    const bool v = inwin && x >= 0 && y >= 0 && x < H && y < W && ((vis >> lane) & 1);
-    const int cell = v ? x * W + y : 0;
-    const uint32_t m = v ? (uint32_t)e.cmap[cell] : 0u;
-    uint32_t tags = 0;  // bit t = tag t (< 16) has a (not suppressed) entity here
-    if ((m & CM_WALL) && !((sup.walls >> lane) & 1)) tags |= 1u << MFG_TAG_WALLS;
-    if (m & CM_DOOR) tags |= 1u << MFG_TAG_DOORS;
-    if (m & CM_ITEM) tags |= 1u << MFG_TAG_ITEMS;
-    if (m & CM_POD) tags |= 1u << MFG_TAG_PODS;
-    if (m & CM_DROP) tags |= 1u << MFG_TAG_DROPOFFS;
-    if (m & CM_DEST) tags |= 1u << MFG_TAG_DESTS;
-    if (m & CM_DIRT) tags |= 1u << MFG_TAG_DIRT;
-    // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
-    if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
-    auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
-      if (!sm) return;
-      bool any = false;
-      for (int i = 0; i < n; i++) {
-        const int w = uni(tbl[i]);
-        any |= v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sm >> i) & 1) && !(dest && (w & EW_REACHED));
-      }
-      tags = any ? (tags | (1u << tag)) : (tags & ~(1u << tag));
-    };
-    resup(e.items(), e.H(H_N_ITEMS), sup.items, MFG_TAG_ITEMS, false);
-    resup(e.pods(), e.H(H_N_PODS), sup.pods, MFG_TAG_PODS, false);
-    resup(e.drops(), e.H(H_N_DROPS), sup.drops, MFG_TAG_DROPOFFS, false);
-    resup(e.dests(), e.H(H_N_DESTS), sup.dests, MFG_TAG_DESTS, true);
-    double dirt_amt = 0.0;
-    if (ballot(m & CM_DIRT)) {  // amount of the (last non-suppressed) pile on the cell
-      bool any = false;
-      for (int i = 0; i < nT; i++) {
-        const int w = uni(e.dirtpos()[i]);
-        const double am = e.dirtamt()[i];
-        if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) { any = true; dirt_amt = am; }
-      }
-      tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
-    }
-    u64 amask = 0;
-    for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
-    // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
-    // 0.4444 open, dirt = amount)
-    auto tagv = [&](int tag) -> double {
-      if (tag >= MFG_TAG_AGENT0) return ((amask >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
-      if (!((tags >> tag) & 1u)) return 0.0;
-      if (tag == MFG_TAG_DOORS) return (m & CM_DCLOSED) ? 0.6666 : 0.4444;
-      if (tag == MFG_TAG_DIRT) return dirt_amt;
-      return 1.0;
-    };
+    wave_sync();
     OT* out_a = out_env + (size_t)a * S->obs_agent_stride;
     const int nl = S->s.n_layers[a];
-    for (int l = 0; l < nl; l++) {
-      const int kind = S->s.layers[a][l].kind;
-      double val = 0.0;
-      if (kind == MFG_LAYER_TAG) {
-        val = tagv(S->s.layers[a][l].tag);
-      } else if (kind == MFG_LAYER_COMBINED) {
-        const int nc = S->s.combined_n[a];
-        for (int q = 0; q < nc; q++) {
-          const double tv = tagv(S->s.combined_tags[a][q]);
-          val = q == 0 ? tv : val + tv;
+    // ---- placement (lane = window cell, 64 cells per pass): tag bits from the cell map ----
+    for (int w0 = 0; w0 < dd; w0 += MFG_WAVE) {
+      const int wi = w0 + lane;
+      const bool inwin = wi < dd;
+      const int x = ax - r + wi / d, y = ay - r + wi % d;
+      const int lx = x - ox + d, ly = y - oy + d;
+      const bool v = inwin && x >= 0 && y >= 0 && x < H && y < W && (unsigned)lx < (unsigned)fw &&
+                     (unsigned)ly < (unsigned)fw && fv[(v_clamp(lx, fw)) * fw + v_clamp(ly, fw)] != 0xFFFFFFFFu;
+      const int cell = v ? x * W + y : 0;
+      const uint32_t m = v ? (uint32_t)e.cmap[cell] : 0u;
+      uint32_t tags = 0;  // bit t = tag t (< 16) has a (not suppressed) entity here
+      if ((m & CM_WALL) && !wsup[inwin ? wi : 0]) tags |= 1u << MFG_TAG_WALLS;
+      if (m & CM_DOOR) tags |= 1u << MFG_TAG_DOORS;
+      if (m & CM_ITEM) tags |= 1u << MFG_TAG_ITEMS;
+      if (m & CM_POD) tags |= 1u << MFG_TAG_PODS;
+      if (m & CM_DROP) tags |= 1u << MFG_TAG_DROPOFFS;
+      if (m & CM_DEST) tags |= 1u << MFG_TAG_DESTS;
+      if (m & CM_DIRT) tags |= 1u << MFG_TAG_DIRT;
+      // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
+      if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
+      auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
+        if (!sm) return;
+        bool any = false;
+        for (int i = 0; i < n; i++) {
+          const int w = uni(tbl[i]);
+          any |= v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sm >> i) & 1) && !(dest && (w & EW_REACHED));
         }
-      } else if (kind == MFG_LAYER_BATTERY) {
-        if (lane == 0) val = frozen ? e.fbat()[a] : e.bat()[a];
-      } else if (kind == MFG_LAYER_GLOBALPOS) {
-        const int gp = frozen ? e.fgp()[a] : apos;
-        if (lane == 0) val = (double)(gp / W) / (double)H;
-        if (lane == 1) val = (double)(gp % W) / (double)W;
+        tags = any ? (tags | (1u << tag)) : (tags & ~(1u << tag));
+      };
+      resup(e.items(), e.H(H_N_ITEMS), sup.items, MFG_TAG_ITEMS, false);
+      resup(e.pods(), e.H(H_N_PODS), sup.pods, MFG_TAG_PODS, false);
+      resup(e.drops(), e.H(H_N_DROPS), sup.drops, MFG_TAG_DROPOFFS, false);
+      resup(e.dests(), e.H(H_N_DESTS), sup.dests, MFG_TAG_DESTS, true);
+      double dirt_amt = 0.0;
+      if (ballot(m & CM_DIRT)) {  // amount of the (last non-suppressed) pile on the cell
+        bool any = false;
+        for (int i = 0; i < nT; i++) {
+          const int w = uni(e.dirtpos()[i]);
+          const double am = e.dirtamt()[i];
+          if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) { any = true; dirt_amt = am; }
+        }
+        tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
       }
-      if (inwin) out_a[(size_t)l * dd + lane] = (OT)val;
+      u64 amask = 0;
+      for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
+      // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
+      // 0.4444 open, dirt = amount)
+      auto tagv = [&](int tag) -> double {
+        if (tag >= MFG_TAG_AGENT0) return ((amask >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
+        if (!((tags >> tag) & 1u)) return 0.0;
+        if (tag == MFG_TAG_DOORS) return (m & CM_DCLOSED) ? 0.6666 : 0.4444;
+        if (tag == MFG_TAG_DIRT) return dirt_amt;
+        return 1.0;
+      };
+      for (int l = 0; l < nl; l++) {
+        const int kind = S->s.layers[a][l].kind;
+        double val = 0.0;
+        if (kind == MFG_LAYER_TAG) {
+          val = tagv(S->s.layers[a][l].tag);
+        } else if (kind == MFG_LAYER_COMBINED) {
+          const int nc = S->s.combined_n[a];
+          for (int q = 0; q < nc; q++) {
+            const double tv = tagv(S->s.combined_tags[a][q]);
+            val = q == 0 ? tv : val + tv;
+          }
+        } else if (kind == MFG_LAYER_BATTERY) {
+          if (wi == 0) val = frozen ? e.fbat()[a] : e.bat()[a];
+        } else if (kind == MFG_LAYER_GLOBALPOS) {
+          const int gp = frozen ? e.fgp()[a] : apos;
+          if (wi == 0) val = (double)(gp / W) / (double)H;
+          if (wi == 1) val = (double)(gp % W) / (double)W;
+        }
+        if (inwin) out_a[(size_t)l * dd + wi] = (OT)val;
+      }
     }
   }
 }
@@ -1947,7 +1938,7 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   if (s->abi_version != MFG_ABI_VERSION) return fail("spec ABI version mismatch");
   if (s->n_agents < 1 || s->n_agents > MFG_MAX_AGENTS) return fail("n_agents out of range");
   if (s->n_doors > MFG_MAX_DOORS) return fail("too many doors");
-  if (s->pomdp_r < 1 || s->pomdp_r > 3) return fail("engine supports pomdp_r in [1,3] (window d*d <= 64 lanes)");
+  if (s->pomdp_r < 1 || s->pomdp_r > 8) return fail("engine supports pomdp_r in [1,8]");
   if (s->H * s->W > 65535) return fail("level too large for 16-bit cell indices");
   if (s->has_machines || s->has_maintainers) return fail("machines/maintainers are not implemented on the device");
   auto* e = new mfg_engine();
@@ -1959,7 +1950,7 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   const int HW = s->H * s->W;
   h.HW = HW; h.nf = s->n_floor; h.nw = s->n_walls; h.nd = s->n_doors; h.A = s->n_agents;
   h.r = s->pomdp_r; h.d = 2 * s->pomdp_r + 1; h.dd = h.d * h.d; h.nrays = s->n_rays;
-  if (h.nrays > 64) { delete e; return fail("more than 64 rays"); }
+  if (h.nrays > 4 * MFG_WAVE) { delete e; return fail("more than 256 rays"); }
   h.maxpts = 2 * s->pomdp_r + 2;
   int lmax = 1;
   for (int a = 0; a < s->n_agents; a++) lmax = s->n_layers[a] > lmax ? s->n_layers[a] : lmax;
@@ -1982,7 +1973,9 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   h.map_bytes = align_up(HW, 16);
   h.lds_full = align_up(h.L.size + 2048 + 4 * MFG_STAB_N, 16);
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
-  h.lds_obs = align_up(h.L.o_mt, 16) + h.map_bytes + 16 * OBS_MAX_PAIRS + align_up(4 * (2 * h.d + 1) * (2 * h.d + 1), 16);
+  h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
+  h.lds_obs = align_up(h.L.o_mt, 16) + h.map_bytes + 16 * OBS_MAX_PAIRS + 4 * h.fv_words + align_up(h.dd, 16) +
+              4 * MFG_WAVE;
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
@@ -2084,6 +2077,11 @@ static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
     case 4: { constexpr int MP = 4; CALL; } break; \
     case 6: { constexpr int MP = 6; CALL; } break; \
     case 8: { constexpr int MP = 8; CALL; } break; \
+    case 10: { constexpr int MP = 10; CALL; } break; \
+    case 12: { constexpr int MP = 12; CALL; } break; \
+    case 14: { constexpr int MP = 14; CALL; } break; \
+    case 16: { constexpr int MP = 16; CALL; } break; \
+    case 18: { constexpr int MP = 18; CALL; } break; \
     default: return fail("unsupported ray length"); \
   }
 

@@ -241,14 +241,14 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
 
     # ---- entities (config_parser.py:80-126), YAML order ----
     ents = cfg.get('Entities') or {}
-    if 'Defaults' in ents:
-        raise UnsupportedSpec('Entities: Defaults')
     group_names = []
     for name in ents:
+        if name == 'Defaults':  # FactoryConfigParser.default_entites is empty (config_parser.py:17,83-85)
+            continue
         if name not in _GROUPS:
             raise UnsupportedSpec(f'entity group {name!r} is not implemented by the engine')
         group_names.append(name)
-    ekw = {k: (v or {}) for k, v in ents.items()}
+    ekw = {k: (v or {}) for k, v in ents.items() if k != 'Defaults'}
     if 'Doors' in ekw and not len(doors):
         raise UnsupportedSpec('Doors requires a D in the level (level_parser.py:492-494)')
 

@@ -22,7 +22,19 @@ def load(tag, seed):
 
 
 def stack_obs(obs_list):
-    return np.stack([np.asarray(x, dtype=np.float64) for x in obs_list])
+    """Per-agent obs (L_a, d, d) f64 -> one array padded with zeros to the largest L (agents may differ)."""
+    xs = [np.asarray(x, dtype=np.float64) for x in obs_list]
+    lmax = max(x.shape[0] for x in xs)
+    out = np.zeros((len(xs), lmax) + xs[0].shape[1:], np.float64)
+    for a, x in enumerate(xs):
+        out[a, :x.shape[0]] = x
+    return out
+
+
+def obs_bytes(obs_list):
+    """Bytes hashed into a fixture's obs_sha: the agents' (L_a, d, d) f64 arrays concatenated in order
+    (for equal L this equals np.stack(...).tobytes())."""
+    return b''.join(np.ascontiguousarray(x, dtype=np.float64).tobytes() for x in obs_list)
 
 
 def info_equal(a, b):

@@ -9,7 +9,8 @@ import pytest
 import golden_compare as G
 
 UNITS = np.load(G.GOLDEN / 'units.npz')
-FIXTURES = [('large8', 'large8.yaml'), ('rooms4', 'rooms4.yaml'), ('simple1', 'simple1.yaml')]
+FIXTURES = [('large8', 'large8.yaml'), ('rooms4', 'rooms4.yaml'), ('simple1', 'simple1.yaml'),
+            ('alltest16', 'alltest16.yaml')]
 
 
 def test_mt19937_matches_cpython():
@@ -92,7 +93,7 @@ def test_oracle_replays_reference_fixture(tag, cfg, seed):
         pc = env.pcg_state()
         if str((int(pc[0]) << 64) | int(pc[1])) != r['pcg']:
             errs.append((t, 'pcg state'))
-        if G.sha(G.stack_obs(obs).tobytes()) != r['obs_sha']:
+        if G.sha(G.obs_bytes(obs)) != r['obs_sha']:
             errs.append((t, 'obs'))
         if len(errs) > 10:
             break

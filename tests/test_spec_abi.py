@@ -24,7 +24,7 @@ def test_compile_headline_spec():
                                  'SpawnEntity(DropOffLocations)', 'SpawnEntity(Inventories)', 'SpawnEntity(Items)']
 
 
-@pytest.mark.parametrize('cfg', ['large8.yaml', 'rooms4.yaml', 'simple1.yaml'])
+@pytest.mark.parametrize('cfg', ['large8.yaml', 'rooms4.yaml', 'simple1.yaml', 'alltest16.yaml'])
 def test_named_action_space_matches_fixture(cfg):
     import golden_compare as G
     from mfg_amd.spec import compile_spec

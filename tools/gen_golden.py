@@ -128,10 +128,16 @@ def run(cfg_name, py_seed, n_steps, action_seed, full_obs_every, level_path=None
                 if 0 <= p[0] < H and 0 <= p[1] < W]
 
     def record(t_global, episode, step, actions, reward, done, info, obs_list, crashed=None):
-        o = np.stack([np.asarray(x, dtype=np.float64) for x in obs_list]) if obs_list else np.zeros(0)
+        xs = [np.asarray(x, dtype=np.float64) for x in obs_list]
+        osha = _h(b''.join(np.ascontiguousarray(x).tobytes() for x in xs))  # agents may differ in L
+        o = np.zeros(0)
+        if xs:
+            o = np.zeros((len(xs), max(x.shape[0] for x in xs)) + xs[0].shape[1:], np.float64)
+            for a, x in enumerate(xs):
+                o[a, :x.shape[0]] = x
         pd = posdict_dump(env, W)
         ent = dict(t=t_global, episode=episode, step=step, actions=actions,
-                   reward=reward, done=done, info=info, obs_sha=_h(o.tobytes()),
+                   reward=reward, done=done, info=info, obs_sha=osha,
                    floor_sha=_h(floor_arr(env, W).tobytes()), posdict_sha=posdict_sha(pd))
         if step <= 3 or t_global % full_obs_every == 0:
             ent['posdict'] = pd
