@@ -170,6 +170,7 @@ typedef struct mfg_events {
   int32_t done_mask;                 /* bit r: rule r produced a VALID DoneResult */
   int32_t crashed;                   /* reference crash path hit (Q17): env flagged, done */
   int32_t step;
+  int32_t maint_base;                /* u_int of the first maintainer (names 'Maintainer[maint_base + k]') */
 } mfg_events;
 
 /* ---- engine ABI (HIP) ---- */

@@ -100,4 +100,5 @@ class MfgEvents(C.Structure):
         ('done_mask', C.c_int32),
         ('crashed', C.c_int32),
         ('step', C.c_int32),
+        ('maint_base', C.c_int32),
     ]

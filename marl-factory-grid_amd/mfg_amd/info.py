@@ -62,6 +62,12 @@ def rebuild_info(spec, actions, ev, reward):
                     info[f'Door[{d}]_Collisions'] += rf[0]
                 dc >>= 1
                 d += 1
+            mc, k = int(g('maint_coll')), 0
+            while mc:  # maintainers of one SpawnEntity call have consecutive u_ints
+                if mc & 1:
+                    info[f"Maintainer[{int(g('maint_base')) + k}]_Collisions"] += rf[0]
+                mc >>= 1
+                k += 1
         elif op in (abi.RULE_BATTERY_DECHARGE, abi.RULE_DONE_BATTERY):
             for a, n in enumerate(names):
                 if watch[a] & 2:
@@ -78,6 +84,10 @@ def rebuild_info(spec, actions, ev, reward):
             info[f'Global_{rname}'] += rf[0]
         elif op == abi.RULE_DONE_DEST:
             info[f'Global_{rname}'] += rf[1]
+        elif op == abi.RULE_DONE_MAINT_COLLISION:  # one DoneResult per agent standing on a maintainer
+            for a, n in enumerate(names):
+                if watch[a] & 4:
+                    info[f'{n}_{rname}'] += rf[0]
     if dm & (1 << 31):
         for op, ri_, rf in spec.rules:
             if op == abi.RULE_WATCH_COLLISIONS:

@@ -69,7 +69,8 @@ _RULES = {
     'DoneAtBatteryDischarge': abi.RULE_DONE_BATTERY, 'DoneAtMaxStepsReached': abi.RULE_DONE_MAXSTEPS,
     'RespawnDirt': abi.RULE_RESPAWN_DIRT, 'EntitiesSmearDirtOnMove': abi.RULE_SMEAR_DIRT,
     'DoneOnAllDirtCleaned': abi.RULE_DONE_DIRT, 'DestinationReachReward': abi.RULE_DEST_REACH,
-    'DoneAtDestinationReach': abi.RULE_DONE_DEST,
+    'DoneAtDestinationReach': abi.RULE_DONE_DEST, 'MoveMaintainers': abi.RULE_MOVE_MAINTAINERS,
+    'DoneAtMaintainerCollision': abi.RULE_DONE_MAINT_COLLISION,
 }
 
 
@@ -388,6 +389,8 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
             rf[0] = float(rkw.get('respawn_amount', 1.0))
         elif op == abi.RULE_DONE_DIRT:
             rf[0] = float(rkw.get('reward', 4.5))
+        elif op == abi.RULE_DONE_MAINT_COLLISION:
+            rf[0] = -5.0  # maintenance/constants.py MAINTAINER_COLLISION_REWARD (the rule takes no kwargs)
         elif op == abi.RULE_DEST_REACH:
             rf[0] = float(rkw.get('dest_reach_reward', 1.0))
         elif op == abi.RULE_DONE_DEST:
@@ -417,8 +420,10 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
         rule_names.append(f'SpawnEntity({g})')
     if len(rules) > abi.MAX_RULES:
         raise UnsupportedSpec('too many rules')
-    if 'Maintainers' in group_names or 'MoveMaintainers' in rules_conf:
-        raise UnsupportedSpec('maintainer pathing is not implemented by the engine yet')
+    if 'MoveMaintainers' in rules_conf and not {'Maintainers', 'Machines', 'Doors'} <= set(group_names):
+        raise UnsupportedSpec('MoveMaintainers needs Maintainers, Machines and Doors (missing groups insert None, Q15)')
+    if 'DoneAtMaintainerCollision' in rules_conf and 'Maintainers' not in group_names:
+        raise UnsupportedSpec('DoneAtMaintainerCollision without Maintainers (Q15)')
     for g, cap_needed in (('Batteries', A), ('GlobalPositions', A)):
         if g in group_names and cap_needed > size + 1:
             raise UnsupportedSpec(f'{g}: {cap_needed} agents exceed LevelParser.size+1={size + 1} (Q16)')
