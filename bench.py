@@ -131,7 +131,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from mfg_amd.spec import compile_spec
-    from mfg_amd.engine import Engine
+    from mfg_amd.engine import Engine, EV_MISC
     from mfg_amd.shard import env_range
 
     spec = compile_spec(args.config)
@@ -144,7 +144,7 @@ def main():
     done = torch.zeros((F, B), dtype=torch.uint8, device=dev)
     ev_a = torch.zeros((F, B, A), dtype=torch.uint8, device=dev)
     ev_w = torch.zeros((F, B, A), dtype=torch.uint8, device=dev)
-    ev_m = torch.zeros((F, B, 10), dtype=torch.int32, device=dev)
+    ev_m = torch.zeros((F, B, EV_MISC), dtype=torch.int32, device=dev)
     eng.reset(obs=obs[0], init=True, seed_base=env_base)
     stream = torch.cuda.current_stream(dev)
     step_no = 0

@@ -17,7 +17,7 @@
 #include "../../include/mfg.h"
 
 #define MFG_WAVE 64
-#define MFG_HDR_N 32
+#define MFG_HDR_N 40
 
 // header slots (int32) of the per-env record
 enum {
@@ -36,6 +36,8 @@ enum {
   H_CNT_AGENT, H_CNT_BATTERY, H_CNT_POD, H_CNT_DROP, H_CNT_ITEM, H_CNT_DIRT, H_CNT_DEST, H_CNT_MACHINE,
   H_CNT_MAINT, H_CNT_GP,
   H_TOTAL_STEPS,   // env-steps since creation (Philox counter)
+  H_N_MACHINES, H_MACHINE_BASE, H_N_MAINTS, H_MAINT_BASE,
+  H_GRAPH_BUILT,   // Gamestate.floortile_graph exists (built once per env lifetime, states.py:82-87)
   H__END
 };
 static_assert(H__END <= MFG_HDR_N, "header overflow");
@@ -64,7 +66,11 @@ struct MfgLayout {
   int32_t o_hdr, o_rule_ctr, o_agent_pos, o_agent_arr, o_agent_par, o_frozen_org, o_frozen_gp;
   int32_t o_door, o_items, o_pods, o_drops, o_dests, o_dirt_pos, o_dirt_id;
   int32_t o_battery, o_frozen_bat, o_dirt_amt, o_pcg, o_mt, o_perm;
+  int32_t o_machines, o_maints;       // lean part: group tables (pos | flags words)
+  int32_t o_mstate, o_mpath, o_grank; // after perm: maintainer state, paths (u16 cells), graph ranks (u16)
 };
+// per-maintainer state ints: [path_n, path_head, next_n, last_serviced, next[mmax + 1]]
+enum { MS_PATH_N = 0, MS_PATH_HEAD, MS_NEXT_N, MS_LAST_SERVICED, MS_NEXT };
 
 struct MfgDevSpec {
   mfg_spec s;  // table pointers inside are HOST pointers: never dereferenced on the device
@@ -81,7 +87,7 @@ struct MfgDevSpec {
   int32_t n_wd_pairs;        // static identifier collisions Wall[k]/Door[k] that one ray fan can reach
   const int32_t* wd_pairs;   // [n_wd_pairs][3]: k, wall cell, door cell
   uint64_t pcg_init_hi, pcg_init_lo, pcg_inc_hi, pcg_inc_lo;  // default_rng(env_seed) state after seeding
-  const uint8_t* base_map;   // [map_bytes] static cell map of the obs render (CM_WALL bits)
+  const uint16_t* base_map;  // [map_bytes / 2] static cell map of the obs render (CM_WALL bits)
   int32_t map_bytes;         // HW rounded up to 16
   int32_t step_rng;          // a rule consumes the floor order / RNG inside a step (dirt spawns)
   MfgLayout L;
@@ -89,6 +95,11 @@ struct MfgDevSpec {
   int32_t lds_logic;         // k_logic: lean record (o_mt bytes) or lds_full when step_rng
   int32_t lds_obs;           // k_obs: lean record + cell map + id-collision pairs + first-visit table + wall sup
   int32_t fv_words;          // first-visit table entries ((2d+1)^2, rounded up to 4)
+  int32_t mmax, kmax;        // machines / maintainers per env (spawn quantities)
+  int32_t mstate_ints, path_cap;  // ints per maintainer state; max stored path length (cells)
+  int32_t bfs_off;           // offset of the BFS scratch in the full-record LDS slice (0 = no maintainers)
+  const int16_t* cell_f;     // [HW] floor index of a cell, -1 for walls
+  const uint8_t* node_ok;    // [nf] floor cell has a floor 8-neighbour (a node of points_to_graph)
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)
   int32_t lds_replay_per_wave;  // k_replay slice: [hdr 128 B][MT 2496 B][perm as u32][shuffle tables]
   int32_t replay_perm_off, replay_sink_off, replay_stab_off, replay_stab_n;

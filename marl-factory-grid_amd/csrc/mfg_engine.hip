@@ -16,6 +16,7 @@
 
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "mfg_device.h"
 
@@ -63,7 +64,8 @@ struct Env {
   uint8_t* lds;     // this wave's LDS slice == image of the HBM record
   int* scratch;     // 512 ints after the record (spawn positions, id-collision pairs)
   uint32_t* stab;   // [MFG_STAB_N] tagged max-tables of the parallel shuffle blocks (not persisted)
-  uint8_t* cmap;    // [HW] per-env cell map of the obs render (rebuilt per render)
+  uint16_t* cmap;   // [HW] per-env cell map of the obs render (rebuilt per render)
+  uint8_t* bfs;     // maintainer BFS scratch (full-record kernels of specs with MoveMaintainers)
   int* hdrp;        // header slots (inside the record image, or a separate slice in k_replay)
   int lane;
   __device__ int* hdr() const { return hdrp; }
@@ -86,6 +88,11 @@ struct Env {
   __device__ uint64_t* pcg() const { return (uint64_t*)(lds + S->L.o_pcg); }
   __device__ uint32_t* mt() const { return (uint32_t*)(lds + S->L.o_mt); }
   __device__ uint16_t* perm() const { return (uint16_t*)(lds + S->L.o_perm); }
+  __device__ int* machines() const { return (int*)(lds + S->L.o_machines); }
+  __device__ int* maints() const { return (int*)(lds + S->L.o_maints); }
+  __device__ int* mst(int k) const { return (int*)(lds + S->L.o_mstate) + k * S->mstate_ints; }
+  __device__ uint16_t* mpath(int k) const { return (uint16_t*)(lds + S->L.o_mpath) + k * S->path_cap; }
+  __device__ uint16_t* grank() const { return (uint16_t*)(lds + S->L.o_grank); }
   // uniform header access
   __device__ int H(int k) const { return uni(hdr()[k]); }
   __device__ void setH(int k, int v) const {
@@ -492,7 +499,8 @@ __device__ __forceinline__ uint32_t philox_u32(uint32_t k0, uint32_t k1, uint32_
 // ------------------------------------------------------------------------------------------------
 // entity model queries (global pos_dict semantics, groups/objects.py:193-214)
 // ------------------------------------------------------------------------------------------------
-enum { K_NONE = -1, K_DOOR = 1, K_ITEM = 3, K_POD = 4, K_DROP = 5, K_DIRT = 6, K_DEST = 7 };
+enum { K_NONE = -1, K_DOOR = 1, K_ITEM = 3, K_POD = 4, K_DROP = 5, K_DIRT = 6, K_DEST = 7, K_MACHINE = 8, K_MAINT = 9,
+       K_WALL = 15 };  // K_WALL: id-collision pair code only (the wall is identified by its cell)
 
 // ballot of group slots at `cell` whose word has all bits of `need`
 __device__ __forceinline__ u64 grp_at(const int* tbl, int n, int cell, int need, int lane) {
@@ -530,6 +538,16 @@ __device__ int find_present_id(const Env& e, int cell, int id, int* slot) {
   const int nd = e.H(H_N_DIRT);
   m = grp_at(e.dirtpos(), nd, cell, EW_PRESENT, lane) & ballot(lane < nd && e.dirtid()[lane < nd ? lane : 0] == id);
   if (m) { *slot = ffs64(m); return K_DIRT; }
+  if (e.S->mmax) {
+    base = e.H(H_MACHINE_BASE);
+    m = grp_at(e.machines(), e.H(H_N_MACHINES), cell, EW_PRESENT, lane) & ballot(base + lane == id);
+    if (m) { *slot = ffs64(m); return K_MACHINE; }
+  }
+  if (e.S->kmax) {
+    base = e.H(H_MAINT_BASE);
+    m = grp_at(e.maints(), e.H(H_N_MAINTS), cell, EW_PRESENT, lane) & ballot(base + lane == id);
+    if (m) { *slot = ffs64(m); return K_MAINT; }
+  }
   return K_NONE;
 }
 // Objects.notify_del_entity x2 on the global pos_dict: list.remove() drops the first identifier-equal entry
@@ -544,6 +562,8 @@ __device__ void global_remove_id(const Env& e, int cell, int id) {
       case K_DROP: e.drops()[slot] &= ~EW_PRESENT; break;
       case K_DEST: e.dests()[slot] &= ~EW_PRESENT; break;
       case K_DIRT: e.dirtpos()[slot] &= ~EW_PRESENT; break;
+      case K_MACHINE: e.machines()[slot] &= ~EW_PRESENT; break;
+      case K_MAINT: e.maints()[slot] &= ~EW_PRESENT; break;
       default: break;
     }
   }
@@ -563,10 +583,14 @@ __device__ bool blocked_at(const Env& e, int cell) {
   bool b = e.lane < A && e.agpos()[e.lane] == cell && e.S->s.agent_blocking[e.lane];
   return ballot(b) != 0;
 }
-// number of colliders in the global list at cell (walls, closed doors, agents)
+// present maintainers at cell (colliders, maintenance/groups.py:11-13)
+__device__ __forceinline__ u64 maints_at(const Env& e, int cell) {
+  return e.S->kmax ? grp_at(e.maints(), e.H(H_N_MAINTS), cell, EW_PRESENT, e.lane) : 0ull;
+}
+// number of colliders in the global list at cell (walls, closed doors, agents, maintainers)
 __device__ int colliders_at(const Env& e, int cell) {
   int n = (e.S->level[cell] == 1) + (present_closed_door(e, cell) ? 1 : 0);
-  return n + popc(agents_at(e, cell));
+  return n + popc(agents_at(e, cell)) + popc(maints_at(e, cell));
 }
 // number of entities in the global list at cell (Door.tick, doors/entitites.py:109)
 __device__ int global_count(const Env& e, int cell) {
@@ -580,6 +604,8 @@ __device__ int global_count(const Env& e, int cell) {
   n += popc(grp_at(e.drops(), e.H(H_N_DROPS), cell, EW_PRESENT, lane));
   n += popc(grp_at(e.dests(), e.H(H_N_DESTS), cell, EW_PRESENT, lane));
   n += popc(grp_at(e.dirtpos(), e.H(H_N_DIRT), cell, EW_PRESENT, lane));
+  if (e.S->mmax) n += popc(grp_at(e.machines(), e.H(H_N_MACHINES), cell, EW_PRESENT, lane));
+  n += popc(maints_at(e, cell));
   return n;
 }
 
@@ -592,6 +618,8 @@ __device__ __forceinline__ bool lane_cell_free(const Env& e, int cell) {
   const int A = e.S->A;
   for (int b = 0; b < A; b++)
     if (e.agpos()[b] == cell) return false;
+  const int nk = e.S->kmax ? e.H(H_N_MAINTS) : 0;
+  for (int i = 0; i < nk; i++) { int w = e.maints()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
   return true;
 }
 // a cell whose global list is empty (empty_positions)
@@ -612,6 +640,10 @@ __device__ __forceinline__ bool lane_cell_empty(const Env& e, int cell) {
   for (int i = 0; i < n; i++) { int w = e.dests()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
   n = e.H(H_N_DIRT);
   for (int i = 0; i < n; i++) { int w = e.dirtpos()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
+  n = e.S->mmax ? e.H(H_N_MACHINES) : 0;
+  for (int i = 0; i < n; i++) { int w = e.machines()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
+  n = e.S->kmax ? e.H(H_N_MAINTS) : 0;
+  for (int i = 0; i < n; i++) { int w = e.maints()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
   return true;
 }
 // first n free cells of a fresh floor shuffle -> out[0..k) (LDS scratch), returns k
@@ -742,6 +774,7 @@ struct StepOut {
   int my_act_ev;      // lane a: act event bits
   int my_watch_ev;    // lane a: watch event bits
   uint64_t door_coll;
+  uint32_t maint_coll;  // maintainers (collection slots) that received a WatchCollisions result
   int respawn_items_value, dirt_spawn_value, dirt_spawn_valid, door_autoclose, done_mask, dest_pack, crashed;
   int done;
 };
@@ -766,6 +799,34 @@ __device__ __forceinline__ void set_agent_pos(const Env& e, int a, int cell) {
 // ------------------------------------------------------------------------------------------------
 // actions (environment/actions.py, modules/*/actions.py)
 // ------------------------------------------------------------------------------------------------
+// DoorUse.do (doors/actions.py:18-34; get_entities_near_pos, global_entities.py:13-38): toggle every door
+// present in the global pos_dict of the 3x3 around (x, y); valid if there was one
+__device__ bool door_use_at(const Env& e, int x, int y) {
+  SpecP S = e.S;
+  const int W = S->s.W;
+  static const int MX[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
+  static const int MY[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
+  u64 toggle = 0;
+  for (int k = 0; k < 9; k++) {
+    const int px = x + MX[k], py = y + MY[k];
+    if (px < 0 || py < 0 || px >= S->s.H || py >= W) continue;
+    const int c = px * W + py;
+    if (S->level[c] == 1) continue;
+    const int d = door_idx(e, c);
+    if (d >= 0 && (e.door()[d] & DW_PRESENT)) toggle |= 1ull << d;
+  }
+  if (!toggle) return false;
+  wave_sync();
+  if (e.lane < S->nd && ((toggle >> e.lane) & 1)) {
+    int w = e.door()[e.lane];
+    if (w & DW_OPEN) w &= ~DW_OPEN;
+    else w = (w & DW_PRESENT) | DW_OPEN | ((S->s.door_auto_close & 0xFF) << 8);
+    e.door()[e.lane] = w;
+  }
+  wave_sync();
+  return true;
+}
+
 __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
   SpecP S = e.S;
   const CS mfg_action& ac = action_of(e, a, slot);
@@ -799,29 +860,8 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
     }
     e.setH(H_DEBT, e.H(H_DEBT) + debt);
     wave_sync();
-  } else if (op == MFG_ACT_DOORUSE) {  // doors/actions.py:18-34; global_entities.py:13-38
-    static const int MX[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
-    static const int MY[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
-    u64 toggle = 0;
-    for (int k = 0; k < 9; k++) {
-      const int px = x + MX[k], py = y + MY[k];
-      if (px < 0 || py < 0 || px >= S->s.H || py >= W) continue;
-      const int c = px * W + py;
-      if (S->level[c] == 1) continue;
-      const int d = door_idx(e, c);
-      if (d >= 0 && (e.door()[d] & DW_PRESENT)) toggle |= 1ull << d;
-    }
-    if (toggle) {
-      valid = 1;
-      wave_sync();
-      if (e.lane < S->nd && ((toggle >> e.lane) & 1)) {
-        int w = e.door()[e.lane];
-        if (w & DW_OPEN) w &= ~DW_OPEN;
-        else w = (w & DW_PRESENT) | DW_OPEN | ((S->s.door_auto_close & 0xFF) << 8);
-        e.door()[e.lane] = w;
-      }
-      wave_sync();
-    }
+  } else if (op == MFG_ACT_DOORUSE) {  // doors/actions.py:18-34
+    valid = door_use_at(e, x, y);
   } else if (op == MFG_ACT_ITEM) {  // items/actions.py:41-63
     if (grp_at(e.drops(), e.H(H_N_DROPS), pos, EW_ALIVE, e.lane)) {
       valid = 0;  // inventories are always empty (pickup bug, Q8)
@@ -878,7 +918,313 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
 // ------------------------------------------------------------------------------------------------
 // rules (environment/rules.py, modules/*/rules.py); hook order states.py:170-226
 // ------------------------------------------------------------------------------------------------
-template <bool RNG>
+// ------------------------------------------------------------------------------------------------
+// maintainers (maintenance/entities.py:17-136, rules.py:9-40) and the floor graph (states.py:82-87)
+// ------------------------------------------------------------------------------------------------
+// one 32-bit MT19937 output (the floor-shuffle debt must be paid first: the stream is shared)
+__device__ uint32_t mt_u32(const Env& e) {
+  int idx = e.H(H_MT_IDX);
+  if (idx >= 624) {
+    mt_twist(e);
+    idx = 0;
+  }
+  const uint32_t y = (uint32_t)uni((int)mt_temper(e.mt()[idx]));
+  e.setH(H_MT_IDX, idx + 1);
+  wave_sync();
+  return y;
+}
+// random._randbelow_with_getrandbits(n) (random.py:239-249), n >= 1
+__device__ int mt_randbelow1(const Env& e, int n) {
+  const int k = 32 - __clz(n);
+  int r = (int)(mt_u32(e) >> (32 - k));
+  while (r >= n) r = (int)(mt_u32(e) >> (32 - k));
+  return r;
+}
+
+#define BFS_ABSENT 0xFFFFu
+#define BFS_ROOT 0xFFFEu
+// neighbours of floor node f in adjacency order: points_to_graph (algorithms/static/utils.py:7-41) adds the
+// edges of itertools.combinations(floorlist, 2) in order, so every adjacency lists its neighbours by
+// ascending build-time rank. nb[k] = rank << 16 | floor index, sorted (a fixed 19-exchange network keeps
+// everything in registers); missing neighbours sort last as 0xFFFFFFFF. Returns the neighbour count.
+__device__ __forceinline__ void cx(uint32_t& a, uint32_t& b) {
+  const uint32_t lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+__device__ __forceinline__ int graph_adj(const Env& e, int f, uint32_t (&nb)[8]) {
+  SpecP S = e.S;
+  const int W = S->s.W, c = S->floor_init[f], x = c / W, y = c % W;
+  const uint16_t* rk = e.grank();
+  int n = 0;
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    const int dx = d < 3 ? -1 : (d == 3 || d == 7 ? 0 : 1);
+    const int dy = (d == 0 || d == 5) ? -1 : ((d == 1 || d == 6) ? 0 : (d == 3 ? -1 : 1));
+    const int nx = x + dx, ny = y + dy;
+    const bool in = nx >= 0 && ny >= 0 && nx < S->s.H && ny < W;
+    const int g = in ? S->cell_f[nx * W + ny] : -1;
+    nb[d] = g >= 0 ? ((uint32_t)rk[g] << 16) | (uint32_t)g : 0xFFFFFFFFu;
+    n += g >= 0;
+  }
+  cx(nb[0], nb[1]); cx(nb[2], nb[3]); cx(nb[4], nb[5]); cx(nb[6], nb[7]);
+  cx(nb[0], nb[2]); cx(nb[1], nb[3]); cx(nb[4], nb[6]); cx(nb[5], nb[7]);
+  cx(nb[1], nb[2]); cx(nb[5], nb[6]); cx(nb[0], nb[4]); cx(nb[3], nb[7]);
+  cx(nb[1], nb[5]); cx(nb[2], nb[6]);
+  cx(nb[1], nb[4]); cx(nb[3], nb[6]);
+  cx(nb[2], nb[4]); cx(nb[3], nb[5]);
+  cx(nb[3], nb[4]);
+  return n;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+// exclusive prefix sum over lanes
+__device__ __forceinline__ int wave_excl_scan(int v, int lane) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+// nx.shortest_path(floortile_graph, src, dst) == nx.bidirectional_shortest_path: networkx 3.4.2
+// _bidirectional_pred_succ restated level-synchronously and exactly. The sequential search visits the
+// candidates (fringe index i, adjacency slot k) of a level in (i, k) order; here every lane expands fringe
+// nodes and the order is recovered from keys i*8+k: the meeting point is the smallest key whose neighbour
+// is in the other tree, a node's parent is its smallest discovering key (LDS atomicMin), and the new fringe
+// is the discoveries compacted in key order. Route (floor indices) into `route`, returns its length or -1
+// (NodeNotFound / NetworkXNoPath / longer than cap: a crash upstream, or engine capacity).
+__device__ int bfs_route(const Env& e, int src, int dst, uint16_t* route, int cap) {
+  SpecP S = e.S;
+  const int nf = S->nf, lane = e.lane;
+  if (!S->node_ok[src] || !S->node_ok[dst]) return -1;
+  if (src == dst) {
+    if (lane == 0) route[0] = (uint16_t)src;
+    wave_sync();
+    return 1;
+  }
+  uint16_t* pred = (uint16_t*)e.bfs;
+  uint16_t* succ = pred + nf;
+  uint16_t* ff = succ + nf;
+  uint16_t* rf = ff + nf;
+  uint16_t* lvl = rf + nf;
+  uint32_t* disc = (uint32_t*)(((uintptr_t)(lvl + nf) + 3) & ~(uintptr_t)3);
+  for (int i = lane; i < nf; i += MFG_WAVE) { pred[i] = BFS_ABSENT; succ[i] = BFS_ABSENT; disc[i] = 0xFFFFFFFFu; }
+  wave_sync();
+  if (lane == 0) { pred[src] = BFS_ROOT; succ[dst] = BFS_ROOT; ff[0] = (uint16_t)src; rf[0] = (uint16_t)dst; }
+  wave_sync();
+  int nff = 1, nrf = 1, meet = -1, level = 0;
+  while (nff && nrf && meet < 0) {
+    const bool fwd = nff <= nrf;
+    uint16_t* F = fwd ? ff : rf;
+    uint16_t* mine = fwd ? pred : succ;
+    const uint16_t* other = fwd ? succ : pred;
+    const int n = fwd ? nff : nrf;
+    for (int i = lane; i < n; i += MFG_WAVE) lvl[i] = F[i];
+    wave_sync();
+    const uint32_t tag = (uint32_t)(4095 - (level & 4095)) << 20;  // newer levels win atomicMin
+    level++;
+    // pass 1: the meeting candidate
+    uint32_t mk = 0xFFFFFFFFu;
+    for (int b = 0; b < n; b += MFG_WAVE) {
+      const int i = b + lane;
+      uint32_t nb[8];
+      const int m = graph_adj(e, lvl[i < n ? i : 0], nb);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (i < n && k < m && other[nb[k] & 0xFFFFu] != BFS_ABSENT) mk = min(mk, (uint32_t)(i * 8 + k));
+    }
+    mk = wave_min_u32(mk);
+    // pass 2: discoveries up to and including the meeting candidate
+    for (int b = 0; b < n; b += MFG_WAVE) {
+      const int i = b + lane;
+      uint32_t nb[8];
+      const int m = graph_adj(e, lvl[i < n ? i : 0], nb);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t key = (uint32_t)(i * 8 + k), g = nb[k] & 0xFFFFu;
+        if (i < n && k < m && key <= mk && mine[g] == BFS_ABSENT) atomicMin(&disc[g], tag | key);
+      }
+    }
+    wave_sync();
+    // pass 3: commit parents; the new fringe in key order
+    int cnt_total = 0;
+    for (int b = 0; b < n; b += MFG_WAVE) {
+      const int i = b + lane;
+      uint32_t nb[8];
+      const int m = graph_adj(e, lvl[i < n ? i : 0], nb);
+      const int vi = i < n ? (int)lvl[i] : 0;
+      uint32_t win = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t key = (uint32_t)(i * 8 + k);
+        if (i < n && k < m && key <= mk && disc[nb[k] & 0xFFFFu] == (tag | key)) win |= 1u << k;
+      }
+      const int cnt = __popc(win);
+      const int off = cnt_total + wave_excl_scan(cnt, lane);
+      int q = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if ((win >> k) & 1u) {
+          mine[nb[k] & 0xFFFFu] = (uint16_t)vi;
+          F[off + q] = (uint16_t)(nb[k] & 0xFFFFu);
+          q++;
+        }
+      }
+      cnt_total += __shfl(off + cnt, 63);
+    }
+    wave_sync();
+    if (mk != 0xFFFFFFFFu) {
+      // the meeting node: neighbour mk & 7 of fringe node mk >> 3
+      uint32_t nb[8];
+      graph_adj(e, lvl[mk >> 3], nb);
+      uint32_t g = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if ((int)(mk & 7u) == k) g = nb[k] & 0xFFFFu;
+      meet = uni((int)g);
+    } else if (fwd) {
+      nff = cnt_total;
+    } else {
+      nrf = cnt_total;
+    }
+  }
+  if (meet < 0) return -1;
+  // path: meet -> pred chain to src (reversed), then the succ chain to dst (lane 0, sequential)
+  int len = 0;
+  if (lane == 0) {
+    int n = 0;
+    for (int w = meet; w != BFS_ROOT && n <= cap; w = pred[w]) n++;
+    int m = 0;
+    for (int w = succ[meet]; w != BFS_ROOT && n + m <= cap; w = succ[w]) m++;
+    len = n + m;
+    if (len <= cap) {
+      int k = n - 1;
+      for (int w = meet; w != BFS_ROOT; w = pred[w]) route[k--] = (uint16_t)w;
+      k = n;
+      for (int w = succ[meet]; w != BFS_ROOT; w = succ[w]) route[k++] = (uint16_t)w;
+    } else {
+      len = -1;
+    }
+  }
+  len = rl(len, 0);
+  wave_sync();
+  return len;
+}
+// Maintainer.calculate_route: route[1:] as cells into the maintainer's path; false on failure
+__device__ bool maint_route(const Env& e, int k, int target_cell, int* crashed) {
+  SpecP S = e.S;
+  int* st = e.mst(k);
+  const int pos = EW_POS(uni(e.maints()[k]));
+  uint16_t* route = (uint16_t*)e.scratch;  // <= 2048 B of scratch: path_cap + 1 <= 1024 cells
+  if (!e.H(H_GRAPH_BUILT)) {  // Gamestate.floortile_graph: points_to_graph(self.entities.floorlist), once
+    pay_debt(e);
+    floor_shuffle(e);
+    for (int i = e.lane; i < S->nf; i += MFG_WAVE) e.grank()[S->cell_f[e.perm()[i]]] = (uint16_t)i;
+    e.setH(H_GRAPH_BUILT, 1);
+    wave_sync();
+  }
+  const int n = bfs_route(e, S->cell_f[pos], S->cell_f[target_cell], route, S->path_cap + 1);
+  if (n < 0) { *crashed = 1; return false; }
+  uint16_t* path = e.mpath(k);
+  for (int i = e.lane; i < n - 1; i += MFG_WAVE) path[i] = (uint16_t)S->floor_init[route[i + 1]];
+  wave_sync();
+  if (e.lane == 0) { st[MS_PATH_N] = n - 1; st[MS_PATH_HEAD] = 0; }
+  wave_sync();
+  return true;
+}
+// Entity.move of maintainer k to `cell` (entity.py:175-199): global pos_dict by identifier (Q14)
+__device__ void maint_move(const Env& e, int k, int cell) {
+  const int id = e.H(H_MAINT_BASE) + k;
+  const int old = EW_POS(uni(e.maints()[k]));
+  global_remove_id(e, old, id);
+  int slot;
+  const bool present = find_present_id(e, cell, id, &slot) == K_NONE;
+  wave_sync();
+  if (e.lane == 0) e.maints()[k] = cell | EW_ALIVE | (present ? EW_PRESENT : 0);
+  wave_sync();
+}
+// Maintainer.tick (maintenance/entities.py:37-62); MoveMaintainers discards every result
+__device__ void maint_tick(const Env& e, int k, int* crashed) {
+  SpecP S = e.S;
+  const int W = S->s.W;
+  int* st = e.mst(k);
+  const int pos = EW_POS(uni(e.maints()[k]));
+  const int nM = e.H(H_N_MACHINES);
+  const u64 mm = grp_at(e.machines(), nM, pos, EW_ALIVE, e.lane);
+  if (mm) {
+    const int mid = e.H(H_MACHINE_BASE) + ffs64(mm);
+    if (mid != uni(st[MS_LAST_SERVICED])) {
+      // MachineAction.do -> Machine.maintain(): idle with health 100 > 98, not valid, no change (Q18)
+      wave_sync();
+      if (e.lane == 0) st[MS_LAST_SERVICED] = mid;
+      wave_sync();
+      return;
+    }
+  }
+  // get_move_action (:64-103)
+  if (uni(st[MS_PATH_HEAD]) >= uni(st[MS_PATH_N])) {
+    int nn = uni(st[MS_NEXT_N]);
+    if (!nn) {
+      pay_debt(e);
+      if (free_positions(e, 1, e.scratch) < 1) { *crashed = 1; return; }  // random_free_position
+      const int fp = uni(e.scratch[0]);
+      int* nx = st + MS_NEXT;
+      if (e.lane == 0) {
+        for (int i = 0; i < nM; i++) nx[i] = EW_POS(e.machines()[i]);
+        nx[nM] = fp;
+      }
+      nn = nM + 1;
+      wave_sync();
+      for (int i = nn - 1; i > 0; i--) {  // shuffle(self._next) (random.py:380-395)
+        const int j = mt_randbelow1(e, i + 1);
+        if (e.lane == 0) { const int t = nx[i]; nx[i] = nx[j]; nx[j] = t; }
+        wave_sync();
+      }
+    }
+    int t = uni(st[MS_NEXT + nn - 1]);
+    nn--;
+    if (!maint_route(e, k, t, crashed)) return;
+    if (uni(st[MS_PATH_N]) == 0) {
+      if (!nn) { *crashed = 1; return; }  // pop from an empty list
+      t = uni(st[MS_NEXT + nn - 1]);
+      nn--;
+      if (!maint_route(e, k, t, crashed)) return;
+    }
+    wave_sync();
+    if (e.lane == 0) st[MS_NEXT_N] = nn;
+    wave_sync();
+  }
+  const int head = uni(st[MS_PATH_HEAD]);
+  if (head >= uni(st[MS_PATH_N])) { *crashed = 1; return; }  // self._path[0] on an empty path
+  const int nxt = uni((int)e.mpath(k)[head]);
+  const int d = door_idx(e, nxt);
+  if (d >= 0 && !(e.door()[d] & DW_OPEN)) {  // _closed_door_in_path -> DoorUse
+    door_use_at(e, pos / W, pos % W);
+    return;
+  }
+  if (colliders_at(e, nxt) > 0) return;  // _predict_move: a collider ahead -> Noop
+  wave_sync();
+  if (e.lane == 0) st[MS_PATH_HEAD] = head + 1;
+  wave_sync();
+  const int dx = nxt / W - pos / W, dy = nxt % W - pos % W;
+  if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || (!dx && !dy)) { *crashed = 1; return; }  // not in MOVEMAP
+  // Move.do (actions.py:77-100): check_move_validity, then Entity.move re-checks (Q3: one shuffle each)
+  if (blocked_at(e, nxt)) return;
+  int debt = 1;
+  if (S->level[nxt] != 1) {
+    debt++;
+    maint_move(e, k, nxt);
+  }
+  e.setH(H_DEBT, e.H(H_DEBT) + debt);
+  wave_sync();
+}
+
+template <bool RNG, bool MAINT>
 __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
   SpecP S = e.S;
   const CS mfg_rule& ru = S->s.rules[ri];
@@ -941,6 +1287,13 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
       if (e.lane == 0) e.rctr()[ri] = c - 1;
       wave_sync();
     }
+  } else if (op == MFG_RULE_MOVE_MAINTAINERS) {  // maintenance/rules.py:16-21
+    if constexpr (RNG && MAINT) {
+      const int nk = e.H(H_N_MAINTS);
+      for (int k = 0; k < nk && !o.crashed; k++) maint_tick(e, k, &o.crashed);
+    } else {
+      o.crashed = 1;  // unreachable: the host launches k_logic<true, true> for specs with MoveMaintainers
+    }
   } else if (op == MFG_RULE_DEST_REACH || op == MFG_RULE_DONE_DEST) {  // destinations/rules.py:34-54
     const int n = e.H(H_N_DESTS);
     for (int i = 0; i < n; i++) {
@@ -980,22 +1333,55 @@ __device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
       wave_sync();
     }
   } else if (op == MFG_RULE_WATCH_COLLISIONS) {  // rules.py:276-307
-    // cells with >= 2 colliders: agent cells (agents, closed doors); every collider there gets one result
+    // Cells with >= 2 colliders (agents, closed doors, maintainers; walls never share a cell). Every collider
+    // there gets one result unless an identifier-equal entity already got one this step. Only int
+    // identifiers can clash (door index vs maintainer u_int), and door cells precede every other floor cell
+    // in the pos_dict key order (walls and doors are keyed first at reset), so door cells are visited first
+    // in door order; the order among the other cells cannot matter.
     const int A = S->A;
+    const int nk = S->kmax ? e.H(H_N_MAINTS) : 0, mbase = S->kmax ? e.H(H_MAINT_BASE) : 0;
     bool hit = false;
+    u64 used = 0;          // int identifiers < 64 that already have a result (door indices, maintainer ids)
+    uint32_t mres = 0;     // maintainers with a result
+    bool agres = false;    // lane a: agent a has a result
+    auto maint_results = [&](int cell) {
+      const u64 mk = maints_at(e, cell);
+      for (u64 m = mk; m; m &= m - 1) {
+        const int k = ffs64(m), id = mbase + k;
+        if ((mres >> k) & 1u) continue;
+        if (id < 64 && ((used >> id) & 1)) continue;
+        mres |= 1u << k;
+        if (id < 64) used |= 1ull << id;
+      }
+    };
+    for (int d = 0; d < S->nd; d++) {
+      const int cell = S->door_cells[d];
+      if (colliders_at(e, cell) < 2) continue;
+      hit = true;
+      if (present_closed_door(e, cell) && !((used >> d) & 1)) { o.door_coll |= 1ull << d; used |= 1ull << d; }
+      if (e.lane < A && e.agpos()[e.lane] == cell) agres = true;
+      maint_results(cell);
+    }
     for (int a = 0; a < A; a++) {
       const int cell = uni(e.agpos()[a]);
-      const int n = colliders_at(e, cell);
-      if (n >= 2) {
-        hit = true;
-        if (e.lane == a) {
-          if (!(o.my_watch_ev & 1)) o.my_rew += ru.f[0];
-          o.my_watch_ev |= 1;
-        }
-        const int d = door_idx(e, cell);
-        if (d >= 0 && present_closed_door(e, cell)) o.door_coll |= 1ull << d;
-      }
+      if (door_idx(e, cell) >= 0 || colliders_at(e, cell) < 2) continue;
+      hit = true;
+      if (e.lane == a) agres = true;
+      maint_results(cell);
     }
+    for (int k = 0; k < nk; k++) {
+      const int w = uni(e.maints()[k]);
+      if (!(w & EW_PRESENT)) continue;
+      const int cell = EW_POS(w);
+      if (door_idx(e, cell) >= 0 || colliders_at(e, cell) < 2) continue;
+      hit = true;
+      maint_results(cell);
+    }
+    if (agres) {
+      if (!(o.my_watch_ev & 1)) o.my_rew += ru.f[0];
+      o.my_watch_ev |= 1;
+    }
+    o.maint_coll |= mres;
     if (ru.i[0] && hit) o.done_mask |= (int)(1u << 31);  // curr_done -> on_check_done
   } else if (op == MFG_RULE_BATTERY_DECHARGE || op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:66-87
     if (e.lane < S->A) {
@@ -1027,6 +1413,15 @@ __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
     const bool any = m != 0;
     const bool all = popc(m) == S->A;
     if (ru.i[1] && (any || all)) { o.done = 1; o.done_mask |= 1 << ri; o.g_rew += ru.f[2]; }
+  } else if (op == MFG_RULE_DONE_MAINT_COLLISION) {  // maintenance/rules.py:32-40
+    const int nk = S->kmax ? e.H(H_N_MAINTS) : 0;
+    bool on = false;
+    if (e.lane < S->A) {
+      const int p = e.agpos()[e.lane];
+      for (int k = 0; k < nk; k++) on |= EW_POS(e.maints()[k]) == p;
+    }
+    if (on) { o.my_rew += ru.f[0]; o.my_watch_ev |= 4; }
+    if (ballot(on)) { o.done = 1; o.done_mask |= 1 << ri; }
   } else if (op == MFG_RULE_DONE_DIRT) {  // clean_up/rules.py:22-25
     if (e.H(H_N_DIRT) == 0 && e.H(H_STEP)) { o.done = 1; o.done_mask |= 1 << ri; o.g_rew += ru.f[0]; }
   } else if (op == MFG_RULE_DONE_DEST) {  // destinations/rules.py:73-92
@@ -1064,6 +1459,12 @@ __device__ void env_reset(const Env& e, int* scratch) {
   e.setH(H_STEP, 0);
   e.setH(H_CRASHED, 0);
   e.setH(H_N_ITEMS, 0); e.setH(H_N_PODS, 0); e.setH(H_N_DROPS, 0); e.setH(H_N_DIRT, 0); e.setH(H_N_DESTS, 0);
+  e.setH(H_N_MACHINES, 0); e.setH(H_N_MAINTS, 0);
+  for (int k = 0; k < S->kmax; k++) {  // maintainers are re-created: no path, no targets, 'None' serviced
+    if (e.lane == 0) {
+      e.mst(k)[MS_PATH_N] = 0; e.mst(k)[MS_PATH_HEAD] = 0; e.mst(k)[MS_NEXT_N] = 0; e.mst(k)[MS_LAST_SERVICED] = -1;
+    }
+  }
   if (e.lane < S->nd) e.door()[e.lane] = DW_PRESENT | ((S->s.door_auto_close & 0xFF) << 8);  // closed
   if (e.lane < A) { e.agpos()[e.lane] = -1; e.agpar()[e.lane] = 0; }
   wave_sync();
@@ -1128,7 +1529,15 @@ __device__ void env_reset(const Env& e, int* scratch) {
     } else if (op == MFG_RULE_SPAWN_GLOBALPOS) {
       e.setH(H_CNT_GP, e.H(H_CNT_GP) + A);
     } else if (op == MFG_RULE_SPAWN_MACHINES || op == MFG_RULE_SPAWN_MAINTAINERS) {
-      e.setH(H_CRASHED, 1);  // not compiled into specs (spec.py rejects), defensive
+      const bool mach = op == MFG_RULE_SPAWN_MACHINES;
+      const int q = ru.i[0];
+      const int n = spawn_positions(e, q, ru.i[1], scratch);
+      const int hn = mach ? H_N_MACHINES : H_N_MAINTS, hc = mach ? H_CNT_MACHINE : H_CNT_MAINT;
+      const int base = e.H(hc);
+      e.setH(mach ? H_MACHINE_BASE : H_MAINT_BASE, base);
+      for (int i = 0; i < n; i++) spawn_into(e, mach ? e.machines() : e.maints(), hn, base, scratch[i]);
+      e.setH(hc, base + n);
+      wave_sync();
     }
     wave_sync();
   }
@@ -1150,6 +1559,8 @@ __device__ void env_reset(const Env& e, int* scratch) {
 #define CM_DROP 32u
 #define CM_DEST 64u    // destination present and not reached
 #define CM_DIRT 128u
+#define CM_MACHINE 256u
+#define CM_MAINT 512u
 
 __device__ __forceinline__ int v_clamp(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
 __device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
@@ -1158,7 +1569,7 @@ __device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
   return (e.cmap[x * S->s.W + y] & (CM_WALL | CM_DCLOSED)) != 0;
 }
 __device__ __forceinline__ void cmap_or(const Env& e, int cell, uint32_t bit) {
-  atomicOr((uint32_t*)(e.cmap + (cell & ~3)), bit << (8 * (cell & 3)));
+  atomicOr((uint32_t*)(e.cmap + (cell & ~1)), bit << (16 * (cell & 1)));
 }
 __device__ void build_cmap(const Env& e) {
   SpecP S = e.S;
@@ -1182,6 +1593,8 @@ __device__ void build_cmap(const Env& e) {
   grp(e.drops(), e.H(H_N_DROPS), CM_DROP, false);
   grp(e.dests(), e.H(H_N_DESTS), CM_DEST, true);
   grp(e.dirtpos(), e.H(H_N_DIRT), CM_DIRT, false);
+  if (S->mmax) grp(e.machines(), e.H(H_N_MACHINES), CM_MACHINE, false);
+  if (S->kmax) grp(e.maints(), e.H(H_N_MAINTS), CM_MAINT, false);
   wave_sync();
 }
 
@@ -1210,14 +1623,17 @@ struct RayLane {
 
 // Identifier-collision candidates (Q14), agent independent, built once per render into scratch:
 // pair q = {cellA, cellB, codeA, codeB}; code = kind << 8 | slot (kind: 1 door, 3 item, 4 pod, 5 drop,
-// 6 dirt, 7 dest, 9 wall -> slot unused, the wall is identified by its cell). Returns the pair count.
+// 6 dirt, 7 dest, 8 machine, 9 maintainer, 15 wall -> slot unused, the wall is identified by its cell).
+// Returns the pair count.
 #define OBS_MAX_PAIRS 120
 __device__ int build_id_pairs(const Env& e, int* pairs) {
   SpecP S = e.S;
   const int lane = e.lane;
   // concatenated dynamic int-id entities: items, pods, drops, dests, dirt (<= 64 in total for dedupe)
   const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
-  const int tot = nI + nP + nR + nS + nT;
+  const int nM = S->mmax ? e.H(H_N_MACHINES) : 0, nK = S->kmax ? e.H(H_N_MAINTS) : 0;
+  const int tot = nI + nP + nR + nS + nT + nM + nK;
+  if (tot > MFG_WAVE) e.setH(H_OVERFLOW, 1);  // more int-id entities than lanes: env flagged, never silent
   int kind = 0, slot = 0, w = 0, id = -1;
   if (lane < tot) {
     int l = lane;
@@ -1225,7 +1641,9 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     else if ((l -= nI) < nP) { kind = K_POD; slot = l; w = e.pods()[l]; id = e.hdr()[H_POD_BASE] + l; }
     else if ((l -= nP) < nR) { kind = K_DROP; slot = l; w = e.drops()[l]; id = e.hdr()[H_DROP_BASE] + l; }
     else if ((l -= nR) < nS) { kind = K_DEST; slot = l; w = e.dests()[l]; id = e.hdr()[H_DEST_BASE] + l; }
-    else { l -= nS; kind = K_DIRT; slot = l; w = e.dirtpos()[l]; id = e.dirtid()[l]; }
+    else if ((l -= nS) < nT) { kind = K_DIRT; slot = l; w = e.dirtpos()[l]; id = e.dirtid()[l]; }
+    else if ((l -= nT) < nM) { kind = K_MACHINE; slot = l; w = e.machines()[l]; id = e.hdr()[H_MACHINE_BASE] + l; }
+    else { l -= nM; kind = K_MAINT; slot = l; w = e.maints()[l]; id = e.hdr()[H_MAINT_BASE] + l; }
     if (!(w & EW_PRESENT)) id = -1;
   }
   const int cell = EW_POS(w);
@@ -1238,7 +1656,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
-      pairs[4 * rank] = cell; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = 9 << 8;
+      pairs[4 * rank] = cell; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = K_WALL << 8;
     }
     n += popc(m);
   }
@@ -1278,7 +1696,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
       pairs[4 * rank] = dc; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = (K_DOOR << 8) | k;
-      pairs[4 * rank + 3] = 9 << 8;
+      pairs[4 * rank + 3] = K_WALL << 8;
     }
     n += popc(m);
   }
@@ -1288,7 +1706,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
 }
 
 struct Sup {  // per-agent suppression sets from the identifier dedupe
-  u64 items, pods, drops, dests, dirt, doors;
+  u64 items, pods, drops, dests, dirt, doors, machines, maints;
   uint8_t* wsup;  // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
   int ax, ay, r, d, W;
 };
@@ -1302,6 +1720,8 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
     case K_DEST: s.dests |= bit; break;
     case K_DIRT: s.dirt |= bit; break;
     case K_DOOR: s.doors |= bit; break;
+    case K_MACHINE: s.machines |= bit; break;
+    case K_MAINT: s.maints |= bit; break;
     default: {
       const int px = (xy >> 16) - s.ax + s.r, py = (xy & 0xFFFF) - s.ay + s.r;
       if (px >= 0 && py >= 0 && px < s.d && py < s.d && lane == 0) s.wsup[px * s.d + py] = 1;
@@ -1374,7 +1794,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     wave_sync();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     Sup sup;
-    sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = 0;
+    sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = sup.machines = sup.maints = 0;
     sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
     sup.wsup = wsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
@@ -1406,7 +1826,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       const bool v = inwin && x >= 0 && y >= 0 && x < H && y < W && (unsigned)lx < (unsigned)fw &&
                      (unsigned)ly < (unsigned)fw && fv[(v_clamp(lx, fw)) * fw + v_clamp(ly, fw)] != 0xFFFFFFFFu;
       const int cell = v ? x * W + y : 0;
-      const uint32_t m = v ? (uint32_t)e.cmap[cell] : 0u;
+      const uint32_t m = v ? (uint32_t)e.cmap[cell] : 0u;  // u16 tag bits
       uint32_t tags = 0;  // bit t = tag t (< 16) has a (not suppressed) entity here
       if ((m & CM_WALL) && !wsup[inwin ? wi : 0]) tags |= 1u << MFG_TAG_WALLS;
       if (m & CM_DOOR) tags |= 1u << MFG_TAG_DOORS;
@@ -1415,6 +1835,8 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       if (m & CM_DROP) tags |= 1u << MFG_TAG_DROPOFFS;
       if (m & CM_DEST) tags |= 1u << MFG_TAG_DESTS;
       if (m & CM_DIRT) tags |= 1u << MFG_TAG_DIRT;
+      if (m & CM_MACHINE) tags |= 1u << MFG_TAG_MACHINES;
+      if (m & CM_MAINT) tags |= 1u << MFG_TAG_MAINTAINERS;
       // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
       if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
       auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
@@ -1430,6 +1852,8 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       resup(e.pods(), e.H(H_N_PODS), sup.pods, MFG_TAG_PODS, false);
       resup(e.drops(), e.H(H_N_DROPS), sup.drops, MFG_TAG_DROPOFFS, false);
       resup(e.dests(), e.H(H_N_DESTS), sup.dests, MFG_TAG_DESTS, true);
+      if (S->mmax) resup(e.machines(), e.H(H_N_MACHINES), sup.machines, MFG_TAG_MACHINES, false);
+      if (S->kmax) resup(e.maints(), e.H(H_N_MAINTS), sup.maints, MFG_TAG_MAINTAINERS, false);
       double dirt_amt = 0.0;
       if (ballot(m & CM_DIRT)) {  // amount of the (last non-suppressed) pile on the cell
         bool any = false;
@@ -1449,6 +1873,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
         if (!((tags >> tag) & 1u)) return 0.0;
         if (tag == MFG_TAG_DOORS) return (m & CM_DCLOSED) ? 0.6666 : 0.4444;
         if (tag == MFG_TAG_DIRT) return dirt_amt;
+        if (tag == MFG_TAG_MACHINES) return (double)S->s.machine_pause;  // idle forever: encoding 15 (Q18)
         return 1.0;
       };
       for (int l = 0; l < nl; l++) {
@@ -1478,13 +1903,13 @@ __device__ void build_obs(const Env& e, OT* out_env) {
 // ------------------------------------------------------------------------------------------------
 // one env-step (Factory.step, factory.py:189-220; Gamestate.tick, states.py:170-203)
 // ------------------------------------------------------------------------------------------------
-#define MFG_EV_MISC 10
+#define MFG_EV_MISC 12
 
-template <bool RNG>
+template <bool RNG, bool MAINT>
 __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   SpecP S = e.S;
   const int A = S->A;
-  o.my_rew = 0.0; o.g_rew = 0.0; o.my_act_ev = 0; o.my_watch_ev = 0; o.door_coll = 0;
+  o.my_rew = 0.0; o.g_rew = 0.0; o.my_act_ev = 0; o.my_watch_ev = 0; o.door_coll = 0; o.maint_coll = 0;
   o.respawn_items_value = -1; o.dirt_spawn_value = -1; o.dirt_spawn_valid = 0; o.door_autoclose = 0;
   o.done_mask = 0; o.dest_pack = 0; o.crashed = 0; o.done = 0;
   e.setH(H_STEP, e.H(H_STEP) + 1);
@@ -1497,7 +1922,7 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   }
   const int nr = S->s.n_rules;
   if (!o.crashed)
-    for (int r = 0; r < nr && !o.crashed; r++) rule_tick_step<RNG>(e, o, r, scratch);
+    for (int r = 0; r < nr && !o.crashed; r++) rule_tick_step<RNG, MAINT>(e, o, r, scratch);
   if (!o.crashed)
     for (int r = 0; r < nr && !o.crashed; r++) rule_post_step(e, o, r);
   if (!o.crashed)
@@ -1535,6 +1960,8 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
       m[7] = o.done_mask;
       m[8] = e.hdr()[H_STEP];
       m[9] = e.hdr()[H_EPISODE];
+      m[10] = (int32_t)o.maint_coll;
+      m[11] = e.S->kmax ? e.hdr()[H_MAINT_BASE] : 0;
     }
   }
 }
@@ -1557,6 +1984,7 @@ __device__ __forceinline__ void env_full(SpecP S, uint8_t* slice, Env& e) {
   e.scratch = (int*)(slice + S->L.size);
   e.stab = (uint32_t*)(slice + S->L.size + 2048);
   e.cmap = nullptr;
+  e.bfs = S->bfs_off ? slice + S->bfs_off : nullptr;
   e.hdrp = (int*)(slice + S->L.o_hdr);
   e.lane = lane_id();
   for (int i = e.lane; i < MFG_STAB_N; i += MFG_WAVE) e.stab[i] = 0u;
@@ -1626,7 +2054,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, ui
 
 // One env-step of every env (no reset, no render). FULL: the spec consumes the floor order inside a
 // step (S->step_rng), so the whole record incl. MT/perm is staged; otherwise only the lean prefix.
-template <bool FULL>
+template <bool FULL, bool MAINT>
 __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, uint8_t* state, long long B,
                                                         const int32_t* actions, unsigned philox_seed,
                                                         unsigned env_base, long long step, double* reward,
@@ -1661,7 +2089,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
     }
   }
   StepOut o;
-  env_step<FULL>(e, my_act, o, e.scratch);
+  env_step<FULL, MAINT>(e, my_act, o, e.scratch);
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
   if (o.done && auto_reset) e.setH(H_DONE, 1);
   wave_sync();
@@ -1700,7 +2128,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, cons
   uint8_t* slice = smem + (size_t)wid * S->lds_obs;
   Env e;
   e.S = S; e.lds = slice; e.stab = nullptr;
-  e.cmap = slice + S->L.o_mt;
+  e.cmap = (uint16_t*)(slice + S->L.o_mt);
   e.scratch = (int*)(slice + S->L.o_mt + S->map_bytes);
   e.hdrp = (int*)(slice + S->L.o_hdr);
   e.lane = lane_id();
@@ -1862,7 +2290,8 @@ static void pcg64_seed(uint32_t entropy, uint64_t* st_hi, uint64_t* st_lo, uint6
 
 static int align_up(int x, int a) { return (x + a - 1) / a * a; }
 
-static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int dropmax, int destmax) {
+static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int dropmax, int destmax, int mmax,
+                        int kmax, int mstate_ints, int path_cap, int graph) {
   int o = 0;
   const int A = s->n_agents, nd = s->n_doors;
   const int dm = s->has_dirt ? MFG_DIRT_MAX : 0;
@@ -1878,6 +2307,8 @@ static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int
   L->o_pods = o; o += 4 * pmax;
   L->o_drops = o; o += 4 * dropmax;
   L->o_dests = o; o += 4 * destmax;
+  L->o_machines = o; o += 4 * mmax;
+  L->o_maints = o; o += 4 * kmax;
   L->o_dirt_pos = o; o += 4 * dm;
   L->o_dirt_id = o; o += 4 * dm;
   o = align_up(o, 8);
@@ -1888,6 +2319,11 @@ static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int
   o = align_up(o, 16);
   L->o_mt = o; o += 4 * 624;
   L->o_perm = o; o += 2 * s->n_floor;
+  o = align_up(o, 4);
+  L->o_mstate = o; o += 4 * kmax * mstate_ints;
+  L->o_mpath = o; o += 2 * kmax * path_cap;
+  o = align_up(o, 4);
+  L->o_grank = o; o += graph ? 2 * s->n_floor : 0;
   L->size = align_up(o, 16);
 }
 
@@ -1940,7 +2376,6 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   if (s->n_doors > MFG_MAX_DOORS) return fail("too many doors");
   if (s->pomdp_r < 1 || s->pomdp_r > 8) return fail("engine supports pomdp_r in [1,8]");
   if (s->H * s->W > 65535) return fail("level too large for 16-bit cell indices");
-  if (s->has_machines || s->has_maintainers) return fail("machines/maintainers are not implemented on the device");
   auto* e = new mfg_engine();
   e->device = device;
   e->B = n_envs;
@@ -1956,22 +2391,32 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   for (int a = 0; a < s->n_agents; a++) lmax = s->n_layers[a] > lmax ? s->n_layers[a] : lmax;
   h.lmax = lmax;
   h.obs_agent_stride = lmax * h.dd;
-  int imax = 0, pmax = 0, dropmax = 0, destmax = 0;
+  int imax = 0, pmax = 0, dropmax = 0, destmax = 0, mmax = 0, kmax = 0, moving = 0;
   for (int r = 0; r < s->n_rules; r++) {
     const mfg_rule& ru = s->rules[r];
     if (ru.op == MFG_RULE_SPAWN_ITEMS) imax = ru.i[0];
     if (ru.op == MFG_RULE_SPAWN_PODS) pmax = ru.i[0];
     if (ru.op == MFG_RULE_SPAWN_DROPOFFS) dropmax = ru.i[0];
     if (ru.op == MFG_RULE_SPAWN_DESTS) destmax = ru.i[0];
+    if (ru.op == MFG_RULE_SPAWN_MACHINES) mmax = ru.i[0];
+    if (ru.op == MFG_RULE_SPAWN_MAINTAINERS) kmax = ru.i[0];
+    if (ru.op == MFG_RULE_MOVE_MAINTAINERS) moving = 1;
   }
-  if (imax > 64 || pmax > 64 || dropmax > 64 || destmax > 64) { delete e; return fail("group quantity > 64"); }
-  h.imax = imax; h.pmax = pmax; h.dropmax = dropmax; h.destmax = destmax;
-  make_layout(s, &h.L, imax, pmax, dropmax, destmax);
+  if (imax > 64 || pmax > 64 || dropmax > 64 || destmax > 64 || mmax > 30 || kmax > 64) {
+    delete e; return fail("group quantity too large for the engine");
+  }
+  h.imax = imax; h.pmax = pmax; h.dropmax = dropmax; h.destmax = destmax; h.mmax = mmax; h.kmax = kmax;
+  h.mstate_ints = MS_NEXT + mmax + 1;
+  h.path_cap = moving ? std::min(std::min(4 * (s->H + s->W), s->n_floor), 1000) : 0;  // route fits the 2 KB scratch
+  make_layout(s, &h.L, imax, pmax, dropmax, destmax, mmax, kmax, h.mstate_ints, h.path_cap, moving);
   h.step_rng = 0;
-  for (int r = 0; r < s->n_rules; r++)
-    if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT) h.step_rng = 1;  // dirt spawns pay the debt mid-step
-  h.map_bytes = align_up(HW, 16);
+  for (int r = 0; r < s->n_rules; r++)  // dirt spawns and maintainer retargets consume the floor order mid-step
+    if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT || s->rules[r].op == MFG_RULE_MOVE_MAINTAINERS) h.step_rng = 1;
+  h.map_bytes = align_up(2 * HW, 16);
   h.lds_full = align_up(h.L.size + 2048 + 4 * MFG_STAB_N, 16);
+  // BFS scratch of the maintainer routing: pred, succ, two fringes, level copy (u16 each) + discovery keys
+  h.bfs_off = moving ? h.lds_full : 0;
+  if (moving) h.lds_full = align_up(h.lds_full + 10 * h.nf + 4 * h.nf + 64, 16);
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
   h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + h.map_bytes + 16 * OBS_MAX_PAIRS + 4 * h.fv_words + align_up(h.dd, 16) +
@@ -1989,7 +2434,18 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   // static tables
   std::vector<uint8_t> door_of(HW, 0xFF);
   for (int d = 0; d < s->n_doors; d++) door_of[s->door_cells[d]] = (uint8_t)d;
-  std::vector<uint8_t> base_map(h.map_bytes, 0);
+  std::vector<int16_t> cell_f(HW, -1);
+  for (int f = 0; f < s->n_floor; f++) cell_f[s->floor_cells[f]] = (int16_t)f;
+  std::vector<uint8_t> node_ok(s->n_floor ? s->n_floor : 1, 0);
+  for (int f = 0; f < s->n_floor; f++) {
+    const int c = s->floor_cells[f], x = c / s->W, y = c % s->W;
+    for (int dx = -1; dx <= 1; dx++)
+      for (int dy = -1; dy <= 1; dy++) {
+        const int nx = x + dx, ny = y + dy;
+        if ((dx || dy) && nx >= 0 && ny >= 0 && nx < s->H && ny < s->W && cell_f[nx * s->W + ny] >= 0) node_ok[f] = 1;
+      }
+  }
+  std::vector<uint16_t> base_map(h.map_bytes / 2, 0);
   for (int c = 0; c < HW; c++)
     if (s->level[c] == 1) base_map[c] = CM_WALL;
   std::vector<int32_t> wd;
@@ -2022,6 +2478,8 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   rc |= upload(e, rp.data(), rp.size(), &h.ray_pts);
   rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
   rc |= upload(e, base_map.data(), base_map.size(), &h.base_map);
+  rc |= upload(e, cell_f.data(), cell_f.size(), &h.cell_f);
+  rc |= upload(e, node_ok.data(), node_ok.size(), &h.node_ok);
   rc |= upload(e, wd.data(), wd.size(), &h.wd_pairs);
   if (rc) { delete e; return -1; }
   if (hipMalloc((void**)&e->d_spec, sizeof(MfgDevSpec)) != hipSuccess ||
@@ -2146,15 +2604,22 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
     const size_t kb = (size_t)k * B;
     {
     PROF_BEGIN(e, st);
-    if (e->h.step_rng) {
-    hipLaunchKernelGGL(k_logic<true>, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+    if (e->h.bfs_off) {
+    hipLaunchKernelGGL((k_logic<true, true>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
+                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
+                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
+                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
+                       auto_reset);
+    } else if (e->h.step_rng) {
+    hipLaunchKernelGGL((k_logic<true, false>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
                        auto_reset);
     } else {
-    hipLaunchKernelGGL(k_logic<false>, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+    hipLaunchKernelGGL((k_logic<false, false>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,

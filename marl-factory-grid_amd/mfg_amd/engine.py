@@ -13,7 +13,8 @@ import numpy as np
 from . import abi
 
 LIB_PATH = Path(os.environ.get('MFG_HIP_LIB') or Path(__file__).resolve().parent / '_lib' / 'libmfg_hip.so')
-EV_MISC = 10
+EV_MISC = 12
+HDR_N = 40  # MFG_HDR_N (csrc/mfg_device.h)
 KERNELS = ['k_logic', 'k_resetdone', 'k_obs', 'k_replay', 'k_reset']  # MFG_K_* ids (include/mfg.h)
 
 LAYOUT_KEYS = ['size', 'o_hdr', 'o_rule_ctr', 'o_agent_pos', 'o_agent_arr', 'o_agent_par', 'o_frozen_org',
@@ -25,7 +26,8 @@ HDR = {k: i for i, k in enumerate([
     'step', 'episode', 'crashed', 'frozen', 'obs_init', 'debt', 'mt_idx', 'n_items', 'n_pods', 'n_drops',
     'n_dirt', 'n_dests', 'item_base', 'pod_base', 'drop_base', 'dest_base', 'bat_base', 'arrival', 'done',
     'overflow', 'cnt_agent', 'cnt_battery', 'cnt_pod', 'cnt_drop', 'cnt_item', 'cnt_dirt', 'cnt_dest',
-    'cnt_machine', 'cnt_maint', 'cnt_gp', 'total_steps'])}
+    'cnt_machine', 'cnt_maint', 'cnt_gp', 'total_steps', 'n_machines', 'machine_base', 'n_maints', 'maint_base',
+    'graph_built'])}
 
 _lib = None
 
@@ -169,7 +171,7 @@ class RecordView:
         return np.frombuffer(self.b, np.float64, n, off)
 
     def hdr(self, k):
-        return int(self.i32(self.L['o_hdr'], 32)[HDR[k]])
+        return int(self.i32(self.L['o_hdr'], HDR_N)[HDR[k]])
 
     def agent_pos(self):
         return self.i32(self.L['o_agent_pos'], self.spec.n_agents)
@@ -206,7 +208,7 @@ def events_from_rows(ev_act, ev_watch, ev_misc):
     m = [int(x) for x in ev_misc]
     dest = [((m[5] >> (8 * k)) & 0xFF) - 1 for k in range(4)]
     return dict(act=[int(x) for x in ev_act], watch=[int(x) for x in ev_watch],
-                door_coll=(m[0] & 0xFFFFFFFF) | ((m[1] & 0xFFFFFFFF) << 32), maint_coll=0,
+                door_coll=(m[0] & 0xFFFFFFFF) | ((m[1] & 0xFFFFFFFF) << 32), maint_coll=m[10] & 0xFFFFFFFF,
                 respawn_items_value=m[2], dirt_spawn_value=m[3], dirt_spawn_valid=m[4],
                 dest_reach_agent=dest, door_autoclose=m[6] & 1, crashed=(m[6] >> 1) & 1, done_mask=m[7],
-                step=m[8])
+                step=m[8], maint_base=m[11])

@@ -19,7 +19,7 @@ import random as _pyrandom
 import numpy as np
 
 from . import abi
-from .engine import Engine, RecordView, events_from_rows, EV_MISC, HDR
+from .engine import Engine, RecordView, events_from_rows, EV_MISC, HDR, HDR_N
 from .info import rebuild_info
 from .spec import compile_spec, UnsupportedSpec
 
@@ -99,7 +99,7 @@ class Factory:
         ver, internal, _ = _pyrandom.getstate()
         words = np.asarray(internal[:624], dtype=np.uint32)
         rec[L['o_mt']:L['o_mt'] + 4 * 624] = words.view(np.uint8)
-        hdr = rec[L['o_hdr']:L['o_hdr'] + 4 * 32].view(np.int32)
+        hdr = rec[L['o_hdr']:L['o_hdr'] + 4 * HDR_N].view(np.int32)
         hdr[HDR['mt_idx']] = int(internal[624])
         self._eng.import_state(self._torch.from_numpy(rec).to(self._dev).reshape(1, -1))
 
