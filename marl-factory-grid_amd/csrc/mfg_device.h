@@ -87,8 +87,9 @@ struct MfgDevSpec {
   int32_t n_wd_pairs;        // static identifier collisions Wall[k]/Door[k] that one ray fan can reach
   const int32_t* wd_pairs;   // [n_wd_pairs][3]: k, wall cell, door cell
   uint64_t pcg_init_hi, pcg_init_lo, pcg_inc_hi, pcg_inc_lo;  // default_rng(env_seed) state after seeding
-  const uint16_t* base_map;  // [map_bytes / 2] static cell map of the obs render (CM_WALL bits)
-  int32_t map_bytes;         // HW rounded up to 16
+  const uint16_t* base_map;  // [map_bytes / 2] static cell map of the obs render (CM_WALL bits), u16 cells
+  const uint8_t* base_map8;  // [map_bytes8] the same with u8 cells (specs without machines/maintainers)
+  int32_t map_bytes, map_bytes8;  // 2*HW / HW rounded up to 16
   int32_t step_rng;          // a rule consumes the floor order / RNG inside a step (dirt spawns)
   MfgLayout L;
   int32_t lds_full;          // bytes of dynamic LDS per wave: full record + scratch + shuffle tables

@@ -64,7 +64,7 @@ struct Env {
   uint8_t* lds;     // this wave's LDS slice == image of the HBM record
   int* scratch;     // 512 ints after the record (spawn positions, id-collision pairs)
   uint32_t* stab;   // [MFG_STAB_N] tagged max-tables of the parallel shuffle blocks (not persisted)
-  uint16_t* cmap;   // [HW] per-env cell map of the obs render (rebuilt per render)
+  uint8_t* cmap;    // [HW] per-env cell map of the obs render (u8 cells, u16 with machines/maintainers)
   uint8_t* bfs;     // maintainer BFS scratch (full-record kernels of specs with MoveMaintainers)
   int* hdrp;        // header slots (inside the record image, or a separate slice in k_replay)
   int lane;
@@ -1563,29 +1563,37 @@ __device__ void env_reset(const Env& e, int* scratch) {
 #define CM_MAINT 512u
 
 __device__ __forceinline__ int v_clamp(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
+template <bool MM>
+__device__ __forceinline__ uint32_t cmap_at(const Env& e, int cell) {
+  return MM ? (uint32_t)((const uint16_t*)e.cmap)[cell] : (uint32_t)e.cmap[cell];
+}
+template <bool MM>
 __device__ __forceinline__ bool light_block(const Env& e, int x, int y) {
   SpecP S = e.S;
   if (x < 0 || y < 0 || x >= S->s.H || y >= S->s.W) return false;
-  return (e.cmap[x * S->s.W + y] & (CM_WALL | CM_DCLOSED)) != 0;
+  return (cmap_at<MM>(e, x * S->s.W + y) & (CM_WALL | CM_DCLOSED)) != 0;
 }
+template <bool MM>
 __device__ __forceinline__ void cmap_or(const Env& e, int cell, uint32_t bit) {
-  atomicOr((uint32_t*)(e.cmap + (cell & ~1)), bit << (16 * (cell & 1)));
+  if (MM) atomicOr((uint32_t*)(e.cmap + 2 * (cell & ~1)), bit << (16 * (cell & 1)));
+  else atomicOr((uint32_t*)(e.cmap + (cell & ~3)), bit << (8 * (cell & 3)));
 }
+template <bool MM>
 __device__ void build_cmap(const Env& e) {
   SpecP S = e.S;
   const int lane = e.lane;
-  const int n16 = S->map_bytes >> 4;
-  const uint4* src = (const uint4*)S->base_map;
+  const int n16 = (MM ? S->map_bytes : S->map_bytes8) >> 4;
+  const uint4* src = MM ? (const uint4*)S->base_map : (const uint4*)S->base_map8;
   for (int i = lane; i < n16; i += MFG_WAVE) ((uint4*)e.cmap)[i] = src[i];
   wave_sync();
   if (lane < S->nd) {
     const int w = e.door()[lane];
-    if (w & DW_PRESENT) cmap_or(e, S->door_cells[lane], CM_DOOR | ((w & DW_OPEN) ? 0u : CM_DCLOSED));
+    if (w & DW_PRESENT) cmap_or<MM>(e, S->door_cells[lane], CM_DOOR | ((w & DW_OPEN) ? 0u : CM_DCLOSED));
   }
   auto grp = [&](const int* tbl, int n, uint32_t bit, bool dest) {
     if (lane < n) {
       const int w = tbl[lane];
-      if ((w & EW_PRESENT) && EW_POS(w) != EW_NOPOS && !(dest && (w & EW_REACHED))) cmap_or(e, EW_POS(w), bit);
+      if ((w & EW_PRESENT) && EW_POS(w) != EW_NOPOS && !(dest && (w & EW_REACHED))) cmap_or<MM>(e, EW_POS(w), bit);
     }
   };
   grp(e.items(), e.H(H_N_ITEMS), CM_ITEM, false);
@@ -1593,8 +1601,8 @@ __device__ void build_cmap(const Env& e) {
   grp(e.drops(), e.H(H_N_DROPS), CM_DROP, false);
   grp(e.dests(), e.H(H_N_DESTS), CM_DEST, true);
   grp(e.dirtpos(), e.H(H_N_DIRT), CM_DIRT, false);
-  if (S->mmax) grp(e.machines(), e.H(H_N_MACHINES), CM_MACHINE, false);
-  if (S->kmax) grp(e.maints(), e.H(H_N_MAINTS), CM_MAINT, false);
+  if (MM && S->mmax) grp(e.machines(), e.H(H_N_MACHINES), CM_MACHINE, false);
+  if (MM && S->kmax) grp(e.maints(), e.H(H_N_MAINTS), CM_MAINT, false);
   wave_sync();
 }
 
@@ -1626,12 +1634,13 @@ struct RayLane {
 // 6 dirt, 7 dest, 8 machine, 9 maintainer, 15 wall -> slot unused, the wall is identified by its cell).
 // Returns the pair count.
 #define OBS_MAX_PAIRS 120
+template <bool MM>
 __device__ int build_id_pairs(const Env& e, int* pairs) {
   SpecP S = e.S;
   const int lane = e.lane;
   // concatenated dynamic int-id entities: items, pods, drops, dests, dirt (<= 64 in total for dedupe)
   const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
-  const int nM = S->mmax ? e.H(H_N_MACHINES) : 0, nK = S->kmax ? e.H(H_N_MAINTS) : 0;
+  const int nM = MM && S->mmax ? e.H(H_N_MACHINES) : 0, nK = MM && S->kmax ? e.H(H_N_MAINTS) : 0;
   const int tot = nI + nP + nR + nS + nT + nM + nK;
   if (tot > MFG_WAVE) e.setH(H_OVERFLOW, 1);  // more int-id entities than lanes: env flagged, never silent
   int kind = 0, slot = 0, w = 0, id = -1;
@@ -1656,7 +1665,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
-      pairs[4 * rank] = cell; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = K_WALL << 8;
+      pairs[3 * rank] = cell; pairs[3 * rank + 1] = wc; pairs[3 * rank + 2] = code | (K_WALL << 24);
     }
     n += popc(m);
   }
@@ -1667,8 +1676,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
-      pairs[4 * rank] = cell; pairs[4 * rank + 1] = dc; pairs[4 * rank + 2] = code;
-      pairs[4 * rank + 3] = (K_DOOR << 8) | id;
+      pairs[3 * rank] = cell; pairs[3 * rank + 1] = dc; pairs[3 * rank + 2] = code | (((K_DOOR << 8) | id) << 16);
     }
     n += popc(m);
   }
@@ -1679,7 +1687,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
-      pairs[4 * rank] = cell; pairs[4 * rank + 1] = cj; pairs[4 * rank + 2] = code; pairs[4 * rank + 3] = codej;
+      pairs[3 * rank] = cell; pairs[3 * rank + 1] = cj; pairs[3 * rank + 2] = code | (codej << 16);
     }
     n += popc(m);
   }
@@ -1695,8 +1703,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
     if (has && rank < OBS_MAX_PAIRS) {
-      pairs[4 * rank] = dc; pairs[4 * rank + 1] = wc; pairs[4 * rank + 2] = (K_DOOR << 8) | k;
-      pairs[4 * rank + 3] = K_WALL << 8;
+      pairs[3 * rank] = dc; pairs[3 * rank + 1] = wc; pairs[3 * rank + 2] = ((K_DOOR << 8) | k) | (K_WALL << 24);
     }
     n += popc(m);
   }
@@ -1730,23 +1737,23 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
   }
 }
 
-template <int MAXPTS, typename OT>
+template <int MAXPTS, typename OT, bool MM>
 __device__ void build_obs(const Env& e, OT* out_env) {
   SpecP S = e.S;
   const int A = S->A, H = S->s.H, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
   const int lane = e.lane;
   const bool frozen = e.H(H_FROZEN) != 0;
-  build_cmap(e);
+  build_cmap<MM>(e);
   int* pairs = e.scratch;
-  const int npairs = build_id_pairs(e, pairs);
+  const int npairs = build_id_pairs<MM>(e, pairs);
   for (int q = lane; q < npairs; q += MFG_WAVE) {  // cells -> packed (x << 16 | y), agent independent
-    const int cA = pairs[4 * q], cB = pairs[4 * q + 1];
-    pairs[4 * q] = ((cA / W) << 16) | (cA % W);
-    pairs[4 * q + 1] = ((cB / W) << 16) | (cB % W);
+    const int cA = pairs[3 * q], cB = pairs[3 * q + 1];
+    pairs[3 * q] = ((cA / W) << 16) | (cA % W);
+    pairs[3 * q + 1] = ((cB / W) << 16) | (cB % W);
   }
   // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
   // ray * 32 + point; it gives both the window visibility and the dedupe order (Q14)
-  uint32_t* fv = (uint32_t*)(e.scratch + 4 * OBS_MAX_PAIRS);
+  uint32_t* fv = (uint32_t*)(e.scratch + 3 * OBS_MAX_PAIRS);
   const int fw = 2 * d + 1, fn = fw * fw;
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
@@ -1773,10 +1780,10 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       for (int p = 0; p < MAXPTS; p++) {
         const int x = ox + ray.dx(p), y = oy + ray.dy(p);
         ing |= (x >= 0 && y >= 0 && x < H && y < W) ? (1u << p) : 0u;
-        blkm |= light_block(e, x, y) ? (1u << p) : 0u;
+        blkm |= light_block<MM>(e, x, y) ? (1u << p) : 0u;
         if (p > 0 && ray.dx(p) != ray.dx(p - 1) && ray.dy(p) != ray.dy(p - 1)) {
           // diagonal step: cut when both orthogonal neighbours block light (ray_caster.py:89-96)
-          const bool c = light_block(e, x, oy + ray.dy(p - 1)) && light_block(e, ox + ray.dx(p - 1), y);
+          const bool c = light_block<MM>(e, x, oy + ray.dy(p - 1)) && light_block<MM>(e, ox + ray.dx(p - 1), y);
           cutm |= c ? (1u << p) : 0u;
         }
       }
@@ -1799,7 +1806,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     sup.wsup = wsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
-      const int pA = q < npairs ? pairs[4 * q] : 0, pB = q < npairs ? pairs[4 * q + 1] : 0;
+      const int pA = q < npairs ? pairs[3 * q] : 0, pB = q < npairs ? pairs[3 * q + 1] : 0;
       const int xA = (pA >> 16) - ox + d, yA = (pA & 0xFFFF) - oy + d;
       const int xB = (pB >> 16) - ox + d, yB = (pB & 0xFFFF) - oy + d;
       const bool nearq = q < npairs && (unsigned)xA < (unsigned)fw && (unsigned)yA < (unsigned)fw &&
@@ -1810,8 +1817,9 @@ __device__ void build_obs(const Env& e, OT* out_env) {
         const int L = ffs64(hm);
         hm &= hm - 1;
         const int qq = q0 + L;
-        if (rl((int)rA, L) < rl((int)rB, L)) sup_add(sup, pairs[4 * qq + 3], rl(pB, L), lane);
-        else sup_add(sup, pairs[4 * qq + 2], rl(pA, L), lane);
+        const int codes = pairs[3 * qq + 2];  // codeA | codeB << 16
+        if (rl((int)rA, L) < rl((int)rB, L)) sup_add(sup, (codes >> 16) & 0xFFFF, rl(pB, L), lane);
+        else sup_add(sup, codes & 0xFFFF, rl(pA, L), lane);
       }
     }
     wave_sync();
@@ -1826,7 +1834,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       const bool v = inwin && x >= 0 && y >= 0 && x < H && y < W && (unsigned)lx < (unsigned)fw &&
                      (unsigned)ly < (unsigned)fw && fv[(v_clamp(lx, fw)) * fw + v_clamp(ly, fw)] != 0xFFFFFFFFu;
       const int cell = v ? x * W + y : 0;
-      const uint32_t m = v ? (uint32_t)e.cmap[cell] : 0u;  // u16 tag bits
+      const uint32_t m = v ? cmap_at<MM>(e, cell) : 0u;
       uint32_t tags = 0;  // bit t = tag t (< 16) has a (not suppressed) entity here
       if ((m & CM_WALL) && !wsup[inwin ? wi : 0]) tags |= 1u << MFG_TAG_WALLS;
       if (m & CM_DOOR) tags |= 1u << MFG_TAG_DOORS;
@@ -1835,8 +1843,8 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       if (m & CM_DROP) tags |= 1u << MFG_TAG_DROPOFFS;
       if (m & CM_DEST) tags |= 1u << MFG_TAG_DESTS;
       if (m & CM_DIRT) tags |= 1u << MFG_TAG_DIRT;
-      if (m & CM_MACHINE) tags |= 1u << MFG_TAG_MACHINES;
-      if (m & CM_MAINT) tags |= 1u << MFG_TAG_MAINTAINERS;
+      if (MM && (m & CM_MACHINE)) tags |= 1u << MFG_TAG_MACHINES;
+      if (MM && (m & CM_MAINT)) tags |= 1u << MFG_TAG_MAINTAINERS;
       // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
       if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
       auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
@@ -1852,8 +1860,8 @@ __device__ void build_obs(const Env& e, OT* out_env) {
       resup(e.pods(), e.H(H_N_PODS), sup.pods, MFG_TAG_PODS, false);
       resup(e.drops(), e.H(H_N_DROPS), sup.drops, MFG_TAG_DROPOFFS, false);
       resup(e.dests(), e.H(H_N_DESTS), sup.dests, MFG_TAG_DESTS, true);
-      if (S->mmax) resup(e.machines(), e.H(H_N_MACHINES), sup.machines, MFG_TAG_MACHINES, false);
-      if (S->kmax) resup(e.maints(), e.H(H_N_MAINTS), sup.maints, MFG_TAG_MAINTAINERS, false);
+      if (MM && S->mmax) resup(e.machines(), e.H(H_N_MACHINES), sup.machines, MFG_TAG_MACHINES, false);
+      if (MM && S->kmax) resup(e.maints(), e.H(H_N_MAINTS), sup.maints, MFG_TAG_MAINTAINERS, false);
       double dirt_amt = 0.0;
       if (ballot(m & CM_DIRT)) {  // amount of the (last non-suppressed) pile on the cell
         bool any = false;
@@ -2115,8 +2123,9 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_
   rec_copy(rec, e.lds, S->L.size, e.lane);
 }
 
-// Observation render of every env into obs[env] (read-only on the state).
-template <int MAXPTS, typename OT>
+// Observation render of every env into obs[env] (read-only on the state). MM: the spec has machines or
+// maintainers (their tags, identifiers and dedupe); compiled out otherwise to keep the VGPR budget.
+template <int MAXPTS, typename OT, bool MM>
 __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                       OT* obs) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2128,14 +2137,14 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, cons
   uint8_t* slice = smem + (size_t)wid * S->lds_obs;
   Env e;
   e.S = S; e.lds = slice; e.stab = nullptr;
-  e.cmap = (uint16_t*)(slice + S->L.o_mt);
-  e.scratch = (int*)(slice + S->L.o_mt + S->map_bytes);
+  e.cmap = slice + S->L.o_mt;
+  e.scratch = (int*)(slice + S->L.o_mt + (MM ? S->map_bytes : S->map_bytes8));
   e.hdrp = (int*)(slice + S->L.o_hdr);
   e.lane = lane_id();
   const uint8_t* rec = state + (size_t)env * S->L.size;
   rec_copy(e.lds, rec, S->L.o_mt, e.lane);
   wave_sync();
-  build_obs<MAXPTS, OT>(e, obs + (size_t)env * S->A * S->obs_agent_stride);
+  build_obs<MAXPTS, OT, MM>(e, obs + (size_t)env * S->A * S->obs_agent_stride);
   if (e.lane == 0 && e.hdrp[H_OVERFLOW]) ((int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_OVERFLOW] = 1;
 }
 
@@ -2413,13 +2422,15 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   for (int r = 0; r < s->n_rules; r++)  // dirt spawns and maintainer retargets consume the floor order mid-step
     if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT || s->rules[r].op == MFG_RULE_MOVE_MAINTAINERS) h.step_rng = 1;
   h.map_bytes = align_up(2 * HW, 16);
+  h.map_bytes8 = align_up(HW, 16);
   h.lds_full = align_up(h.L.size + 2048 + 4 * MFG_STAB_N, 16);
   // BFS scratch of the maintainer routing: pred, succ, two fringes, level copy (u16 each) + discovery keys
   h.bfs_off = moving ? h.lds_full : 0;
   if (moving) h.lds_full = align_up(h.lds_full + 10 * h.nf + 4 * h.nf + 64, 16);
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
   h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
-  h.lds_obs = align_up(h.L.o_mt, 16) + h.map_bytes + 16 * OBS_MAX_PAIRS + 4 * h.fv_words + align_up(h.dd, 16) +
+  h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) + 12 * OBS_MAX_PAIRS +
+              4 * h.fv_words + align_up(h.dd, 16) +
               4 * MFG_WAVE;
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
@@ -2446,8 +2457,9 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
       }
   }
   std::vector<uint16_t> base_map(h.map_bytes / 2, 0);
+  std::vector<uint8_t> base_map8(h.map_bytes8, 0);
   for (int c = 0; c < HW; c++)
-    if (s->level[c] == 1) base_map[c] = CM_WALL;
+    if (s->level[c] == 1) { base_map[c] = CM_WALL; base_map8[c] = CM_WALL; }
   std::vector<int32_t> wd;
   const int reach = 2 * s->pomdp_r + 1;
   for (int k = 0; k < s->n_walls && k < s->n_doors; k++) {
@@ -2478,6 +2490,7 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   rc |= upload(e, rp.data(), rp.size(), &h.ray_pts);
   rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
   rc |= upload(e, base_map.data(), base_map.size(), &h.base_map);
+  rc |= upload(e, base_map8.data(), base_map8.size(), &h.base_map8);
   rc |= upload(e, cell_f.data(), cell_f.size(), &h.cell_f);
   rc |= upload(e, node_ok.data(), node_ok.size(), &h.node_ok);
   rc |= upload(e, wd.data(), wd.size(), &h.wd_pairs);
@@ -2525,8 +2538,12 @@ static unsigned env_grid(const mfg_engine* e) { return (unsigned)((e->B + MFG_WP
 
 template <int MP, typename OT>
 static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
-  hipLaunchKernelGGL((k_obs<MP, OT>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_obs * MFG_WPB, st,
-                     e->d_spec, e->d_state, (long long)e->B, obs);
+  if (e->h.mmax || e->h.kmax)
+    hipLaunchKernelGGL((k_obs<MP, OT, true>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_obs * MFG_WPB,
+                       st, e->d_spec, e->d_state, (long long)e->B, obs);
+  else
+    hipLaunchKernelGGL((k_obs<MP, OT, false>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_obs * MFG_WPB,
+                       st, e->d_spec, e->d_state, (long long)e->B, obs);
   return hipGetLastError();
 }
 
