@@ -102,6 +102,6 @@ struct MfgDevSpec {
   const int16_t* cell_f;     // [HW] floor index of a cell, -1 for walls
   const uint8_t* node_ok;    // [nf] floor cell has a floor 8-neighbour (a node of points_to_graph)
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)
-  int32_t lds_replay_per_wave;  // k_replay slice: [hdr 128 B][MT 2496 B][perm as u32][shuffle tables]
-  int32_t replay_perm_off, replay_sink_off, replay_stab_off, replay_stab_n;
+  int32_t lds_replay_per_wave;  // k_replay slice: [hdr][MT + u16 perm image of the record][sink][tables]
+  int32_t replay_mtperm, replay_sink_off, replay_stab_off, replay_stab_n;
 };

@@ -323,13 +323,28 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
   return first_j;
 }
 
+// 16-bit exchange in LDS: ds_mskor_rtn_b32 (MEM = (MEM & ~mask) | data, returns the old word) on the
+// aligned word holding `p`, so a floor permutation can stay u16 in LDS. Conflicting lanes of one
+// instruction are applied in lane order (probed by mfg_create, k_probe_xchg).
+__device__ __forceinline__ uint32_t lds_xchg_u16(uint16_t* p, uint32_t v) {
+  const uint32_t a = (uint32_t)(uintptr_t)p;  // low 32 bits of a generic LDS address = the LDS offset
+  const uint32_t sh = (a & 2u) << 3;
+  const uint32_t mask = 0xFFFFu << sh, data = (v & 0xFFFFu) << sh;
+  uint32_t old;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(old)
+               : "v"(a & ~3u), "v"(mask), "v"(data)
+               : "memory");
+  return (old >> sh) & 0xFFFFu;
+}
+
 // k_replay's shuffle: the exchange path of mt_randbelow_seq specialised for the replay kernel (64
-// draws per chunk, 32-bit perm). Out-of-play lanes read and write a per-lane sink word instead of
+// draws per chunk, the record's own u16 permutation, 16-bit exchanges). Out-of-play lanes read and write a per-lane sink word instead of
 // branching, so a block runs without exec-mask changes. stab: [64] rank table (tag << 6 | lane),
 // [64] chunk counter.
 #define RP_CTR 64
 #define RP_STAB_N 68
-__device__ void replay_shuffle(const Env& e, uint32_t* perm) {
+__device__ void replay_shuffle(const Env& e, uint16_t* perm) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
   uint32_t* sink = (uint32_t*)e.scratch + lane;
@@ -383,7 +398,7 @@ __device__ void replay_shuffle(const Env& e, uint32_t* perm) {
     if (nacc) {
       const int imin = icur - nacc + 1;
       const int i = icur - A, j = (int)r;
-      uint32_t* pi = acc ? &perm[i] : sink;
+      uint16_t* pi = acc ? &perm[i] : (uint16_t*)sink;
       const int P0 = (int)*pi;
       ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
       const uint32_t tag = ctr << 6;
@@ -399,9 +414,9 @@ __device__ void replay_shuffle(const Env& e, uint32_t* perm) {
         if (ptr >= 0) { v = v2; ptr = p2; }
       }
       // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j]
-      const uint32_t F = atomicExch(acc ? &perm[j] : sink, (uint32_t)v);
+      const uint32_t F = lds_xchg_u16(acc ? &perm[j] : (uint16_t*)sink, (uint32_t)v);
       wave_sync();
-      *pi = F;
+      *pi = (uint16_t)F;
       wave_sync();
     }
 #endif
@@ -2169,39 +2184,29 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   e.stab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_stab_off);
   e.hdrp = (int*)(smem + (size_t)wid * S->lds_replay_per_wave);
   int* hdr = e.hdr();
-  uint32_t* p32 = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_perm_off);
-  const int nf = S->nf;
-  // header: lanes copy 32 ints; MT: 16 B per lane; perm: u16 pairs widened to u32
+  const int n16 = S->replay_mtperm >> 4;  // MT + u16 perm image of the record, 16 B units
   if (e.lane < MFG_HDR_N) hdr[e.lane] = ((const int*)(rec + S->L.o_hdr))[e.lane];
   {
     const uint4* src = (const uint4*)(rec + S->L.o_mt);
     uint4* dst = (uint4*)(e.lds + S->L.o_mt);
-    for (int i = e.lane; i < 624 / 4; i += MFG_WAVE) dst[i] = src[i];
-    const uint32_t* ps = (const uint32_t*)(rec + S->L.o_perm);
-    for (int i = e.lane; 2 * i < nf; i += MFG_WAVE) {
-      const uint32_t w = ps[i];
-      p32[2 * i] = w & 0xFFFFu;
-      p32[2 * i + 1] = w >> 16;
-    }
+    for (int i = e.lane; i < n16; i += MFG_WAVE) dst[i] = src[i];
   }
   for (int i = e.lane; i < S->replay_stab_n; i += MFG_WAVE) e.stab[i] = 0u;
   wave_sync();
   if (S->xchg_ordered) {
 #ifndef MFG_ABLATE_NODEBT
     const int debt = e.H(H_DEBT);
-    for (int k = 0; k < debt; k++) replay_shuffle(e, p32);
+    for (int k = 0; k < debt; k++) replay_shuffle(e, e.perm());
 #endif
     e.setH(H_DEBT, 0);
     wave_sync();
   } else {
-    pay_debt_t(e, p32);
+    pay_debt(e);
   }
   {
     const uint4* src = (const uint4*)(e.lds + S->L.o_mt);
     uint4* dst = (uint4*)(rec + S->L.o_mt);
-    for (int i = e.lane; i < 624 / 4; i += MFG_WAVE) dst[i] = src[i];
-    uint32_t* pd = (uint32_t*)(rec + S->L.o_perm);
-    for (int i = e.lane; 2 * i < nf; i += MFG_WAVE) pd[i] = (p32[2 * i] & 0xFFFFu) | (p32[2 * i + 1] << 16);
+    for (int i = e.lane; i < n16; i += MFG_WAVE) dst[i] = src[i];
   }
   if (e.lane == 0) {
     ((int*)(rec + S->L.o_hdr))[H_DEBT] = 0;
@@ -2361,6 +2366,25 @@ __global__ void __launch_bounds__(64) k_probe_xchg(int* bad) {
     nbad += (old != want) + (tab[lane] != want_fin);
     wave_sync();
   }
+  // the same for 16-bit exchanges through ds_mskor_rtn_b32 (two entries per word, both halves conflict)
+  __shared__ uint16_t tab16[64];
+  for (int it = 1; it <= 64; it++) {
+    tab16[lane] = (uint16_t)(1000 + lane);
+    wave_sync();
+    const int a = (int)((lane * 2246822519u + it * 3266489917u) >> 9) % it;
+    const uint32_t old = lds_xchg_u16(&tab16[a], (uint32_t)lane);
+    wave_sync();
+    int prev = -1;
+    for (int l = 0; l < lane; l++)
+      if ((int)((l * 2246822519u + it * 3266489917u) >> 9) % it == a) prev = l;
+    const uint32_t want = prev >= 0 ? (uint32_t)prev : 1000u + a;
+    int last = -1;
+    for (int l = 0; l < 64; l++)
+      if ((int)((l * 2246822519u + it * 3266489917u) >> 9) % it == lane) last = l;
+    const uint32_t want_fin = last >= 0 ? (uint32_t)last : 1000u + lane;
+    nbad += (old != want) + ((uint32_t)tab16[lane] != want_fin);
+    wave_sync();
+  }
   atomicAdd(bad, nbad);
 }
 
@@ -2435,8 +2459,8 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
-    h.replay_perm_off = 4 * MFG_HDR_N + 4 * 624;
-    h.replay_sink_off = h.replay_perm_off + align_up(4 * (h.nf + 1), 16);
+    h.replay_mtperm = align_up(4 * 624 + 2 * h.nf, 16);  // o_perm == o_mt + 2496 (make_layout)
+    h.replay_sink_off = 4 * MFG_HDR_N + h.replay_mtperm;
     h.replay_stab_off = h.replay_sink_off + 4 * MFG_WAVE;
     h.replay_stab_n = h.xchg_ordered ? RP_STAB_N : MFG_STAB_N;
     h.lds_replay_per_wave = align_up(h.replay_stab_off + 4 * h.replay_stab_n, 16);
