@@ -430,7 +430,15 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
 
 // random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
 template <typename PT>
-__device__ __forceinline__ void floor_shuffle_t(const Env& e, PT* perm) { mt_randbelow_seq(e, e.S->nf - 1, 1, perm); }
+__device__ __forceinline__ void floor_shuffle_t(const Env& e, PT* perm) {
+  if constexpr (sizeof(PT) == 2) {
+    if (e.S->xchg_ordered) {  // the branch-free exchange path (the replay kernel's) whenever it is probed
+      replay_shuffle(e, perm);
+      return;
+    }
+  }
+  mt_randbelow_seq(e, e.S->nf - 1, 1, perm);
+}
 __device__ __forceinline__ void floor_shuffle(const Env& e) { floor_shuffle_t(e, e.perm()); }
 
 // Pay the shuffle debt accumulated by membership-only floorlist calls (check_pos_validity, Q3).
