@@ -42,7 +42,7 @@ enum {
 };
 static_assert(H__END <= MFG_HDR_N, "header overflow");
 
-#define MFG_DIRT_MAX 64
+#define MFG_DIRT_MAX 1024  // dirt-pile slots per env: MfgDevSpec::dirt_cap (<= this) is sized per spec
 
 // shuffle-block tables in LDS (u32): [rank table 64][counter][pad 3][j-hash table 512 (table path only)]
 #define MFG_STAB_HASH 512
@@ -98,7 +98,12 @@ struct MfgDevSpec {
   int32_t fv_words;          // first-visit table entries ((2d+1)^2, rounded up to 4)
   int32_t mmax, kmax;        // machines / maintainers per env (spawn quantities)
   int32_t mstate_ints, path_cap;  // ints per maintainer state; max stored path length (cells)
-  int32_t bfs_off;           // offset of the BFS scratch in the full-record LDS slice (0 = no maintainers)
+  int32_t bfs_off;           // offset of the BFS scratch in the full-record LDS slice (0 = none or in HBM)
+  int32_t bfs_bytes;         // BFS scratch bytes per env (pred, succ, 2 fringes, level copy u16 + keys u32)
+  uint8_t* bfs_pool;         // [B][bfs_bytes] BFS scratch in HBM when it does not fit the LDS slice, else null
+  int32_t dirt_cap;          // dirt-pile slots per env record (spawn budget of one episode, multiple of 64)
+  int32_t scratch_bytes;     // per-wave LDS scratch after the record (spawn positions + amounts, routes)
+  int32_t max_pairs;         // capacity of the obs identifier-collision pair list (bounded by group sizes)
   const int16_t* cell_f;     // [HW] floor index of a cell, -1 for walls
   const uint8_t* node_ok;    // [nf] floor cell has a floor 8-neighbour (a node of points_to_graph)
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)

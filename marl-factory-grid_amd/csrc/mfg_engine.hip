@@ -530,6 +530,19 @@ __device__ __forceinline__ u64 grp_at(const int* tbl, int n, int cell, int need,
   int w = lane < n ? tbl[lane] : 0;
   return ballot(lane < n && EW_POS(w) == cell && (w & need) == need);
 }
+// groups longer than a wave (dirt piles): lowest matching slot / number of matching slots, 64 per pass
+__device__ __forceinline__ int grp_first(const int* tbl, int n, int cell, int need, int lane) {
+  for (int b = 0; b < n; b += MFG_WAVE) {
+    const u64 m = grp_at(tbl + b, n - b, cell, need, lane);
+    if (m) return b + ffs64(m);
+  }
+  return -1;
+}
+__device__ __forceinline__ int grp_count(const int* tbl, int n, int cell, int need, int lane) {
+  int c = 0;
+  for (int b = 0; b < n; b += MFG_WAVE) c += popc(grp_at(tbl + b, n - b, cell, need, lane));
+  return c;
+}
 __device__ __forceinline__ u64 agents_at(const Env& e, int cell) {
   const int A = e.S->A;
   int p = e.lane < A ? e.agpos()[e.lane] : -1;
@@ -559,8 +572,11 @@ __device__ int find_present_id(const Env& e, int cell, int id, int* slot) {
   m = grp_at(e.dests(), e.H(H_N_DESTS), cell, EW_PRESENT, lane) & ballot(base + lane == id);
   if (m) { *slot = ffs64(m); return K_DEST; }
   const int nd = e.H(H_N_DIRT);
-  m = grp_at(e.dirtpos(), nd, cell, EW_PRESENT, lane) & ballot(lane < nd && e.dirtid()[lane < nd ? lane : 0] == id);
-  if (m) { *slot = ffs64(m); return K_DIRT; }
+  for (int b = 0; b < nd; b += MFG_WAVE) {
+    const int i = b + lane;
+    m = grp_at(e.dirtpos() + b, nd - b, cell, EW_PRESENT, lane) & ballot(i < nd && e.dirtid()[i < nd ? i : 0] == id);
+    if (m) { *slot = b + ffs64(m); return K_DIRT; }
+  }
   if (e.S->mmax) {
     base = e.H(H_MACHINE_BASE);
     m = grp_at(e.machines(), e.H(H_N_MACHINES), cell, EW_PRESENT, lane) & ballot(base + lane == id);
@@ -626,7 +642,7 @@ __device__ int global_count(const Env& e, int cell) {
   n += popc(grp_at(e.pods(), e.H(H_N_PODS), cell, EW_PRESENT, lane));
   n += popc(grp_at(e.drops(), e.H(H_N_DROPS), cell, EW_PRESENT, lane));
   n += popc(grp_at(e.dests(), e.H(H_N_DESTS), cell, EW_PRESENT, lane));
-  n += popc(grp_at(e.dirtpos(), e.H(H_N_DIRT), cell, EW_PRESENT, lane));
+  n += grp_count(e.dirtpos(), e.H(H_N_DIRT), cell, EW_PRESENT, lane);
   if (e.S->mmax) n += popc(grp_at(e.machines(), e.H(H_N_MACHINES), cell, EW_PRESENT, lane));
   n += popc(maints_at(e, cell));
   return n;
@@ -729,29 +745,29 @@ __device__ int dirt_trigger_spawn(const Env& e, int q, double amount, int* valid
   int n_new = (int)fabs((double)q + u);
   pay_debt(e);
   int npos = free_positions(e, n_new, scratch);
-  // amounts: drawn for range(q) before any placement (numpy PCG64)
-  const int qa = q < MFG_WAVE ? q : MFG_WAVE;
-  double my_amt = amount;
-  for (int i = 0; i < qa; i++) {
+  int n = npos < q ? npos : q;
+  // amounts: drawn for range(q) before any placement (numpy PCG64); the first n are kept in scratch
+  // after the positions (scratch_bytes is sized for both at the spec's largest spawn)
+  double* amts = (double*)(scratch + ((n + 1) & ~1));
+  for (int i = 0; i < q; i++) {
     double a = amount != 0.0 ? amount : s.dirt_initial_amount + pcg_uniform(e, -s.dirt_amount_var, s.dirt_amount_var);
-    if (e.lane == i) my_amt = a;
+    if (e.lane == 0 && i < n) amts[i] = a;
   }
-  int n = npos < qa ? npos : qa;
+  wave_sync();
   int counter = 0;
   for (int i = 0; i < n; i++) {
     const int cell = scratch[i];
-    const double a = __shfl(my_amt, i);
+    const double a = amts[i];
     if (dirt_global_amount(e) > s.dirt_max_global) { *valid = 0; return counter; }
     const int nd = e.H(H_N_DIRT);
-    u64 m = grp_at(e.dirtpos(), nd, cell, EW_ALIVE, e.lane);
-    if (m) {
-      const int k = ffs64(m);
+    const int k = grp_first(e.dirtpos(), nd, cell, EW_ALIVE, e.lane);
+    if (k >= 0) {
       double nv = e.dirtamt()[k] + a;
       wave_sync();
       if (e.lane == 0) e.dirtamt()[k] = nv < DIRTPILE_MAX_LOCAL ? nv : DIRTPILE_MAX_LOCAL;
       wave_sync();
     } else {
-      if (nd >= MFG_DIRT_MAX) { e.setH(H_OVERFLOW, 1); *valid = 0; return counter; }
+      if (nd >= e.S->dirt_cap) { e.setH(H_OVERFLOW, 1); *valid = 0; return counter; }
       int id = e.H(H_CNT_DIRT);
       int slot;
       bool present = find_present_id(e, cell, id, &slot) == K_NONE;
@@ -776,13 +792,15 @@ __device__ void dirt_delete(const Env& e, int k) {
   const int cell = EW_POS(e.dirtpos()[k]);
   const int id = e.dirtid()[k];
   global_remove_id(e, cell, id);
-  int p = 0, i = 0;
-  double a = 0.0;
-  if (e.lane < nd && e.lane != k) { p = e.dirtpos()[e.lane]; i = e.dirtid()[e.lane]; a = e.dirtamt()[e.lane]; }
-  wave_sync();
-  if (e.lane < nd && e.lane != k) {
-    int dst = e.lane > k ? e.lane - 1 : e.lane;
-    e.dirtpos()[dst] = p; e.dirtid()[dst] = i; e.dirtamt()[dst] = a;
+  for (int b = k & ~(MFG_WAVE - 1); b < nd; b += MFG_WAVE) {  // shift slots k+1.. down by one, 64 per pass
+    const int j = b + e.lane;
+    const bool mv = j > k && j < nd;
+    int p = 0, i = 0;
+    double a = 0.0;
+    if (mv) { p = e.dirtpos()[j]; i = e.dirtid()[j]; a = e.dirtamt()[j]; }
+    wave_sync();
+    if (mv) { e.dirtpos()[j - 1] = p; e.dirtid()[j - 1] = i; e.dirtamt()[j - 1] = a; }
+    wave_sync();
   }
   e.setH(H_N_DIRT, nd - 1);
   wave_sync();
@@ -913,9 +931,8 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
       }
     }
   } else if (op == MFG_ACT_CLEAN) {  // clean_up/actions.py:19-36
-    u64 m = grp_at(e.dirtpos(), e.H(H_N_DIRT), pos, EW_PRESENT, e.lane);
-    if (m) {
-      const int k = ffs64(m);
+    const int k = grp_first(e.dirtpos(), e.H(H_N_DIRT), pos, EW_PRESENT, e.lane);
+    if (k >= 0) {
       const double na = e.dirtamt()[k] - S->s.dirt_clean_amount;
       if (na <= 0) {
         dirt_delete(e, k);
@@ -1014,6 +1031,12 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane) {
   }
   return x - v;
 }
+// BFS scratch may live in HBM (e.bfs in the per-env pool): lanes exchange through it after a
+// workgroup-scope fence (s_waitcnt on both LDS and vector memory), not just the wave barrier
+__device__ __forceinline__ void bfs_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
 // nx.shortest_path(floortile_graph, src, dst) == nx.bidirectional_shortest_path: networkx 3.4.2
 // _bidirectional_pred_succ restated level-synchronously and exactly. The sequential search visits the
 // candidates (fringe index i, adjacency slot k) of a level in (i, k) order; here every lane expands fringe
@@ -1027,7 +1050,7 @@ __device__ int bfs_route(const Env& e, int src, int dst, uint16_t* route, int ca
   if (!S->node_ok[src] || !S->node_ok[dst]) return -1;
   if (src == dst) {
     if (lane == 0) route[0] = (uint16_t)src;
-    wave_sync();
+    bfs_sync();
     return 1;
   }
   uint16_t* pred = (uint16_t*)e.bfs;
@@ -1037,9 +1060,9 @@ __device__ int bfs_route(const Env& e, int src, int dst, uint16_t* route, int ca
   uint16_t* lvl = rf + nf;
   uint32_t* disc = (uint32_t*)(((uintptr_t)(lvl + nf) + 3) & ~(uintptr_t)3);
   for (int i = lane; i < nf; i += MFG_WAVE) { pred[i] = BFS_ABSENT; succ[i] = BFS_ABSENT; disc[i] = 0xFFFFFFFFu; }
-  wave_sync();
+  bfs_sync();
   if (lane == 0) { pred[src] = BFS_ROOT; succ[dst] = BFS_ROOT; ff[0] = (uint16_t)src; rf[0] = (uint16_t)dst; }
-  wave_sync();
+  bfs_sync();
   int nff = 1, nrf = 1, meet = -1, level = 0;
   while (nff && nrf && meet < 0) {
     const bool fwd = nff <= nrf;
@@ -1048,7 +1071,7 @@ __device__ int bfs_route(const Env& e, int src, int dst, uint16_t* route, int ca
     const uint16_t* other = fwd ? succ : pred;
     const int n = fwd ? nff : nrf;
     for (int i = lane; i < n; i += MFG_WAVE) lvl[i] = F[i];
-    wave_sync();
+    bfs_sync();
     const uint32_t tag = (uint32_t)(4095 - (level & 4095)) << 20;  // newer levels win atomicMin
     level++;
     // pass 1: the meeting candidate
@@ -1073,7 +1096,7 @@ __device__ int bfs_route(const Env& e, int src, int dst, uint16_t* route, int ca
         if (i < n && k < m && key <= mk && mine[g] == BFS_ABSENT) atomicMin(&disc[g], tag | key);
       }
     }
-    wave_sync();
+    bfs_sync();
     // pass 3: commit parents; the new fringe in key order
     int cnt_total = 0;
     for (int b = 0; b < n; b += MFG_WAVE) {
@@ -1098,9 +1121,9 @@ __device__ int bfs_route(const Env& e, int src, int dst, uint16_t* route, int ca
           q++;
         }
       }
-      cnt_total += __shfl(off + cnt, 63);
+      cnt_total = __shfl(off + cnt, 63);  // off already includes the earlier passes
     }
-    wave_sync();
+    bfs_sync();
     if (mk != 0xFFFFFFFFu) {
       // the meeting node: neighbour mk & 7 of fringe node mk >> 3
       uint32_t nb[8];
@@ -1135,7 +1158,7 @@ __device__ int bfs_route(const Env& e, int src, int dst, uint16_t* route, int ca
     }
   }
   len = rl(len, 0);
-  wave_sync();
+  bfs_sync();
   return len;
 }
 // Maintainer.calculate_route: route[1:] as cells into the maintainer's path; false on failure
@@ -1143,7 +1166,7 @@ __device__ bool maint_route(const Env& e, int k, int target_cell, int* crashed) 
   SpecP S = e.S;
   int* st = e.mst(k);
   const int pos = EW_POS(uni(e.maints()[k]));
-  uint16_t* route = (uint16_t*)e.scratch;  // <= 2048 B of scratch: path_cap + 1 <= 1024 cells
+  uint16_t* route = (uint16_t*)e.scratch;  // scratch_bytes >= 2 * (path_cap + 2)
   if (!e.H(H_GRAPH_BUILT)) {  // Gamestate.floortile_graph: points_to_graph(self.entities.floorlist), once
     pay_debt(e);
     floor_shuffle(e);
@@ -1152,7 +1175,7 @@ __device__ bool maint_route(const Env& e, int k, int target_cell, int* crashed) 
     wave_sync();
   }
   const int n = bfs_route(e, S->cell_f[pos], S->cell_f[target_cell], route, S->path_cap + 1);
-  if (n < 0) { *crashed = 1; return false; }
+  if (n < 0) { *crashed = 2; return false; }  // NodeNotFound / NetworkXNoPath (or route > path_cap)
   uint16_t* path = e.mpath(k);
   for (int i = e.lane; i < n - 1; i += MFG_WAVE) path[i] = (uint16_t)S->floor_init[route[i + 1]];
   wave_sync();
@@ -1194,7 +1217,7 @@ __device__ void maint_tick(const Env& e, int k, int* crashed) {
     int nn = uni(st[MS_NEXT_N]);
     if (!nn) {
       pay_debt(e);
-      if (free_positions(e, 1, e.scratch) < 1) { *crashed = 1; return; }  // random_free_position
+      if (free_positions(e, 1, e.scratch) < 1) { *crashed = 3; return; }  // random_free_position
       const int fp = uni(e.scratch[0]);
       int* nx = st + MS_NEXT;
       if (e.lane == 0) {
@@ -1213,7 +1236,7 @@ __device__ void maint_tick(const Env& e, int k, int* crashed) {
     nn--;
     if (!maint_route(e, k, t, crashed)) return;
     if (uni(st[MS_PATH_N]) == 0) {
-      if (!nn) { *crashed = 1; return; }  // pop from an empty list
+      if (!nn) { *crashed = 4; return; }  // pop from an empty list
       t = uni(st[MS_NEXT + nn - 1]);
       nn--;
       if (!maint_route(e, k, t, crashed)) return;
@@ -1223,7 +1246,7 @@ __device__ void maint_tick(const Env& e, int k, int* crashed) {
     wave_sync();
   }
   const int head = uni(st[MS_PATH_HEAD]);
-  if (head >= uni(st[MS_PATH_N])) { *crashed = 1; return; }  // self._path[0] on an empty path
+  if (head >= uni(st[MS_PATH_N])) { *crashed = 5; return; }  // self._path[0] on an empty path
   const int nxt = uni((int)e.mpath(k)[head]);
   const int d = door_idx(e, nxt);
   if (d >= 0 && !(e.door()[d] & DW_OPEN)) {  // _closed_door_in_path -> DoorUse
@@ -1235,7 +1258,7 @@ __device__ void maint_tick(const Env& e, int k, int* crashed) {
   if (e.lane == 0) st[MS_PATH_HEAD] = head + 1;
   wave_sync();
   const int dx = nxt / W - pos / W, dy = nxt % W - pos % W;
-  if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || (!dx && !dy)) { *crashed = 1; return; }  // not in MOVEMAP
+  if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || (!dx && !dy)) { *crashed = 6; return; }  // not in MOVEMAP
   // Move.do (actions.py:77-100): check_move_validity, then Entity.move re-checks (Q3: one shuffle each)
   if (blocked_at(e, nxt)) return;
   int debt = 1;
@@ -1614,8 +1637,8 @@ __device__ void build_cmap(const Env& e) {
     if (w & DW_PRESENT) cmap_or<MM>(e, S->door_cells[lane], CM_DOOR | ((w & DW_OPEN) ? 0u : CM_DCLOSED));
   }
   auto grp = [&](const int* tbl, int n, uint32_t bit, bool dest) {
-    if (lane < n) {
-      const int w = tbl[lane];
+    for (int i = lane; i < n; i += MFG_WAVE) {
+      const int w = tbl[i];
       if ((w & EW_PRESENT) && EW_POS(w) != EW_NOPOS && !(dest && (w & EW_REACHED))) cmap_or<MM>(e, EW_POS(w), bit);
     }
   };
@@ -1653,66 +1676,67 @@ struct RayLane {
 };
 
 // Identifier-collision candidates (Q14), agent independent, built once per render into scratch:
-// pair q = {cellA, cellB, codeA, codeB}; code = kind << 8 | slot (kind: 1 door, 3 item, 4 pod, 5 drop,
-// 6 dirt, 7 dest, 8 machine, 9 maintainer, 15 wall -> slot unused, the wall is identified by its cell).
-// Returns the pair count.
-#define OBS_MAX_PAIRS 120
+// pair q = {cellA, cellB, codeA | codeB << 16}; code = kind << 12 | slot (kind: 1 door, 3 item, 4 pod,
+// 5 drop, 6 dirt, 7 dest, 8 machine, 9 maintainer, 15 wall -> slot unused, the wall is identified by its
+// cell). The dynamic int-id entities are the concatenation items, pods, drops, dests, dirt, machines,
+// maintainers, handled 64 per pass. Returns the pair count (<= S->max_pairs, a bound from the group sizes).
+struct IdEnt {
+  int kind, slot, cell, id;
+};
+template <bool MM>
+__device__ __forceinline__ IdEnt id_entity(const Env& e, int l, int nI, int nP, int nR, int nS, int nT, int nM, int tot) {
+  IdEnt r{0, 0, 0, -1};
+  if (l >= tot) return r;
+  int w;
+  if (l < nI) { r.kind = K_ITEM; r.slot = l; w = e.items()[l]; r.id = e.hdr()[H_ITEM_BASE] + l; }
+  else if ((l -= nI) < nP) { r.kind = K_POD; r.slot = l; w = e.pods()[l]; r.id = e.hdr()[H_POD_BASE] + l; }
+  else if ((l -= nP) < nR) { r.kind = K_DROP; r.slot = l; w = e.drops()[l]; r.id = e.hdr()[H_DROP_BASE] + l; }
+  else if ((l -= nR) < nS) { r.kind = K_DEST; r.slot = l; w = e.dests()[l]; r.id = e.hdr()[H_DEST_BASE] + l; }
+  else if ((l -= nS) < nT) { r.kind = K_DIRT; r.slot = l; w = e.dirtpos()[l]; r.id = e.dirtid()[l]; }
+  else if (!MM) { w = 0; }
+  else if ((l -= nT) < nM) { r.kind = K_MACHINE; r.slot = l; w = e.machines()[l]; r.id = e.hdr()[H_MACHINE_BASE] + l; }
+  else { l -= nM; r.kind = K_MAINT; r.slot = l; w = e.maints()[l]; r.id = e.hdr()[H_MAINT_BASE] + l; }
+  if (!(w & EW_PRESENT)) r.id = -1;
+  r.cell = EW_POS(w);
+  return r;
+}
 template <bool MM>
 __device__ int build_id_pairs(const Env& e, int* pairs) {
   SpecP S = e.S;
-  const int lane = e.lane;
-  // concatenated dynamic int-id entities: items, pods, drops, dests, dirt (<= 64 in total for dedupe)
+  const int lane = e.lane, cap = S->max_pairs;
   const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
   const int nM = MM && S->mmax ? e.H(H_N_MACHINES) : 0, nK = MM && S->kmax ? e.H(H_N_MAINTS) : 0;
   const int tot = nI + nP + nR + nS + nT + nM + nK;
-  if (tot > MFG_WAVE) e.setH(H_OVERFLOW, 1);  // more int-id entities than lanes: env flagged, never silent
-  int kind = 0, slot = 0, w = 0, id = -1;
-  if (lane < tot) {
-    int l = lane;
-    if (l < nI) { kind = K_ITEM; slot = l; w = e.items()[l]; id = e.hdr()[H_ITEM_BASE] + l; }
-    else if ((l -= nI) < nP) { kind = K_POD; slot = l; w = e.pods()[l]; id = e.hdr()[H_POD_BASE] + l; }
-    else if ((l -= nP) < nR) { kind = K_DROP; slot = l; w = e.drops()[l]; id = e.hdr()[H_DROP_BASE] + l; }
-    else if ((l -= nR) < nS) { kind = K_DEST; slot = l; w = e.dests()[l]; id = e.hdr()[H_DEST_BASE] + l; }
-    else if ((l -= nS) < nT) { kind = K_DIRT; slot = l; w = e.dirtpos()[l]; id = e.dirtid()[l]; }
-    else if ((l -= nT) < nM) { kind = K_MACHINE; slot = l; w = e.machines()[l]; id = e.hdr()[H_MACHINE_BASE] + l; }
-    else { l -= nM; kind = K_MAINT; slot = l; w = e.maints()[l]; id = e.hdr()[H_MAINT_BASE] + l; }
-    if (!(w & EW_PRESENT)) id = -1;
-  }
-  const int cell = EW_POS(w);
-  const int code = (kind << 8) | slot;
   int n = 0;
-  // wall partner
-  {
-    const bool has = id >= 0 && id < S->nw;
-    const int wc = has ? S->wall_cells[id] : 0;
+  auto emit = [&](bool has, int cA, int cB, int codes) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
-    if (has && rank < OBS_MAX_PAIRS) {
-      pairs[3 * rank] = cell; pairs[3 * rank + 1] = wc; pairs[3 * rank + 2] = code | (K_WALL << 24);
-    }
+    if (has && rank < cap) { pairs[3 * rank] = cA; pairs[3 * rank + 1] = cB; pairs[3 * rank + 2] = codes; }
     n += popc(m);
-  }
-  // door partner
-  {
-    const bool has = id >= 0 && id < S->nd && (e.door()[id < S->nd && id >= 0 ? id : 0] & DW_PRESENT);
-    const int dc = has ? S->door_cells[id] : 0;
-    const u64 m = ballot(has);
-    const int rank = n + mbcnt(m);
-    if (has && rank < OBS_MAX_PAIRS) {
-      pairs[3 * rank] = cell; pairs[3 * rank + 1] = dc; pairs[3 * rank + 2] = code | (((K_DOOR << 8) | id) << 16);
+  };
+  for (int b = 0; b < tot; b += MFG_WAVE) {
+    const IdEnt me = id_entity<MM>(e, b + lane, nI, nP, nR, nS, nT, nM, tot);
+    const int code = (me.kind << 12) | me.slot;
+    {  // wall partner Wall[id]
+      const bool has = me.id >= 0 && me.id < S->nw;
+      emit(has, me.cell, has ? S->wall_cells[me.id] : 0, code | (K_WALL << 28));
     }
-    n += popc(m);
-  }
-  // dynamic-dynamic partners (different kinds, equal identifiers): lane l pairs with every later lane
-  for (int j = 0; j < tot && j < MFG_WAVE; j++) {
-    const int idj = rl(id, j), kj = rl(kind, j), cj = rl(cell, j), codej = rl(code, j);
-    const bool has = lane < j && id >= 0 && idj == id && kj != kind;
-    const u64 m = ballot(has);
-    const int rank = n + mbcnt(m);
-    if (has && rank < OBS_MAX_PAIRS) {
-      pairs[3 * rank] = cell; pairs[3 * rank + 1] = cj; pairs[3 * rank + 2] = code | (codej << 16);
+    {  // door partner Door[id]
+      const bool has = me.id >= 0 && me.id < S->nd && (e.door()[me.id < S->nd && me.id >= 0 ? me.id : 0] & DW_PRESENT);
+      emit(has, me.cell, has ? S->door_cells[me.id] : 0, code | (((K_DOOR << 12) | me.id) << 16));
     }
-    n += popc(m);
+    // dynamic-dynamic partners (different kinds, equal identifiers): entity b+lane pairs with every later one
+    for (int j = b + 1; j < tot; j++) {
+      IdEnt o;
+      if (j < b + MFG_WAVE) {
+        const int jl = j - b;
+        o.kind = rl(me.kind, jl); o.slot = rl(me.slot, jl); o.cell = rl(me.cell, jl); o.id = rl(me.id, jl);
+      } else {
+        o = id_entity<MM>(e, j, nI, nP, nR, nS, nT, nM, tot);
+      }
+      const bool has = b + lane < j && me.id >= 0 && o.id == me.id && o.kind != me.kind;
+      emit(has, me.cell, o.cell, code | (((o.kind << 12) | o.slot) << 16));
+    }
   }
   // static Wall[k] / Door[k] pairs (host-filtered to pairs one ray fan can reach)
   for (int q0 = 0; q0 < S->n_wd_pairs; q0 += MFG_WAVE) {
@@ -1723,32 +1747,34 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
       k = S->wd_pairs[3 * q]; wc = S->wd_pairs[3 * q + 1]; dc = S->wd_pairs[3 * q + 2];
       has = (e.door()[k] & DW_PRESENT) != 0;
     }
-    const u64 m = ballot(has);
-    const int rank = n + mbcnt(m);
-    if (has && rank < OBS_MAX_PAIRS) {
-      pairs[3 * rank] = dc; pairs[3 * rank + 1] = wc; pairs[3 * rank + 2] = ((K_DOOR << 8) | k) | (K_WALL << 24);
-    }
-    n += popc(m);
+    emit(has, dc, wc, ((K_DOOR << 12) | k) | (K_WALL << 28));
   }
-  if (n > OBS_MAX_PAIRS) e.setH(H_OVERFLOW, 1);
+  if (n > cap) e.setH(H_OVERFLOW, 1);
   wave_sync();
-  return n < OBS_MAX_PAIRS ? n : OBS_MAX_PAIRS;
+  return n < cap ? n : cap;
 }
 
 struct Sup {  // per-agent suppression sets from the identifier dedupe
   u64 items, pods, drops, dests, dirt, doors, machines, maints;
-  uint8_t* wsup;  // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
+  uint8_t* wsup;   // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
+  uint32_t* dsup;  // dirt slots >= 64: LDS bitmap [dirt_cap / 32] (null when dirt_cap <= 64)
   int ax, ay, r, d, W;
+  __device__ __forceinline__ bool dirt_sup(int i) const {
+    return dsup ? ((dsup[i >> 5] >> (i & 31)) & 1u) != 0 : ((dirt >> (i & 63)) & 1ull) != 0;
+  }
 };
 __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
-  const int kind = code >> 8, slot = code & 0xFF;
+  const int kind = code >> 12, slot = code & 0xFFF;
   const u64 bit = 1ull << (slot & 63);
   switch (kind) {
     case K_ITEM: s.items |= bit; break;
     case K_POD: s.pods |= bit; break;
     case K_DROP: s.drops |= bit; break;
     case K_DEST: s.dests |= bit; break;
-    case K_DIRT: s.dirt |= bit; break;
+    case K_DIRT:
+      if (s.dsup) { if (lane == 0) s.dsup[slot >> 5] |= 1u << (slot & 31); }
+      else s.dirt |= bit;
+      break;
     case K_DOOR: s.doors |= bit; break;
     case K_MACHINE: s.machines |= bit; break;
     case K_MAINT: s.maints |= bit; break;
@@ -1776,10 +1802,13 @@ __device__ void build_obs(const Env& e, OT* out_env) {
   }
   // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
   // ray * 32 + point; it gives both the window visibility and the dedupe order (Q14)
-  uint32_t* fv = (uint32_t*)(e.scratch + 3 * OBS_MAX_PAIRS);
+  uint32_t* fv = (uint32_t*)(e.scratch + 3 * S->max_pairs);
   const int fw = 2 * d + 1, fn = fw * fw;
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
+  // dirt suppression bitmap for groups wider than a wave: after the per-lane sink words of the ray walk
+  uint32_t* dsup = S->dirt_cap > MFG_WAVE ? (uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE : nullptr;
+  const int ndsup = S->dirt_cap >> 5;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
   const int agp = lane < A ? e.agpos()[lane] : -1;
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
@@ -1792,6 +1821,8 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     const int ox = org / W, oy = org % W;
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
+    if (dsup)
+      for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
     wave_sync();
     // ---- ray walk (lane = ray, 64 rays per pass): blocking bits first, then the walk on bitmasks ----
     for (int pass = 0; pass < npass; pass++) {
@@ -1827,6 +1858,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = sup.machines = sup.maints = 0;
     sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
     sup.wsup = wsup;
+    sup.dsup = dsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
       const int pA = q < npairs ? pairs[3 * q] : 0, pB = q < npairs ? pairs[3 * q + 1] : 0;
@@ -1891,7 +1923,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
         for (int i = 0; i < nT; i++) {
           const int w = uni(e.dirtpos()[i]);
           const double am = e.dirtamt()[i];
-          if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !((sup.dirt >> i) & 1)) { any = true; dirt_amt = am; }
+          if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !sup.dirt_sup(i)) { any = true; dirt_amt = am; }
         }
         tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
       }
@@ -1960,10 +1992,10 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
     for (int r = 0; r < nr; r++) rule_check_done(e, o, r);
   // the step's membership-only shuffles stay as debt: paid by k_replay after the launch, or inline by
   // the next order-dependent consumer (spawn / reset)
-  if (o.crashed || e.H(H_OVERFLOW)) {
+  if (o.crashed || e.H(H_OVERFLOW)) {  // H_CRASHED keeps the reason: 1 rule/action crash upstream, 2-6 maintainer
+    e.setH(H_CRASHED, o.crashed ? o.crashed : 7);  // (route, free cell, next, path, move), 7 capacity overflow
     o.crashed = 1;
     o.done = 1;
-    e.setH(H_CRASHED, 1);
   }
   wave_sync();
 }
@@ -2006,16 +2038,17 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
 //   k_obs       observation render; LDS = lean record + cell map + id-collision pairs; read-only on state
 // and k_replay pays the accumulated floor-shuffle debt once per mfg_step call.
 // ------------------------------------------------------------------------------------------------
-#define MFG_WPB 4
+#define MFG_LDS_MAX 163840  // LDS bytes per CU on gfx950 (one workgroup may use all of it)
+#define MFG_WPB 4  // waves (envs) per workgroup at most; fewer when a slice is large (wpb_for)
 
-// full-record slice: [record][scratch 2 KB][shuffle tables]
-__device__ __forceinline__ void env_full(SpecP S, uint8_t* slice, Env& e) {
+// full-record slice: [record][scratch][shuffle tables][BFS scratch if it fits]
+__device__ __forceinline__ void env_full(SpecP S, uint8_t* slice, Env& e, long long env) {
   e.S = S;
   e.lds = slice;
   e.scratch = (int*)(slice + S->L.size);
-  e.stab = (uint32_t*)(slice + S->L.size + 2048);
+  e.stab = (uint32_t*)(slice + S->L.size + S->scratch_bytes);
   e.cmap = nullptr;
-  e.bfs = S->bfs_off ? slice + S->bfs_off : nullptr;
+  e.bfs = S->bfs_pool ? S->bfs_pool + (size_t)env * S->bfs_bytes : (S->bfs_off ? slice + S->bfs_off : nullptr);
   e.hdrp = (int*)(slice + S->L.o_hdr);
   e.lane = lane_id();
   for (int i = e.lane; i < MFG_STAB_N; i += MFG_WAVE) e.stab[i] = 0u;
@@ -2032,11 +2065,11 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, ui
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = threadIdx.x >> 6;
-  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
   if (mask && !mask[env]) return;
   Env e;
-  env_full(S, smem + (size_t)wid * S->lds_full, e);
+  env_full(S, smem + (size_t)wid * S->lds_full, e, env);
   uint8_t* rec = state + (size_t)env * S->L.size;
   if (init & MFG_INIT_CREATE) {
     if (init & MFG_INIT_KEEP_MT) {
@@ -2094,13 +2127,13 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = threadIdx.x >> 6;
-  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
   Env e;
   uint8_t* slice = smem + (size_t)wid * S->lds_logic;
   constexpr bool full = FULL;
   if (full) {
-    env_full(S, slice, e);
+    env_full(S, slice, e, env);
   } else {
     e.S = S; e.lds = slice; e.scratch = nullptr; e.stab = nullptr; e.cmap = nullptr;
     e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
@@ -2132,12 +2165,12 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = threadIdx.x >> 6;
-  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
   uint8_t* rec = state + (size_t)env * S->L.size;
   if (uni(((const int*)(rec + S->L.o_hdr))[H_DONE]) == 0) return;
   Env e;
-  env_full(S, smem + (size_t)wid * S->lds_full, e);
+  env_full(S, smem + (size_t)wid * S->lds_full, e, env);
   rec_copy(e.lds, rec, S->L.size, e.lane);
   wave_sync();
   env_reset(e, e.scratch);
@@ -2154,7 +2187,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, cons
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = threadIdx.x >> 6;
-  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
   // slice: [lean record][cell map][pairs]
   uint8_t* slice = smem + (size_t)wid * S->lds_obs;
@@ -2177,7 +2210,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = threadIdx.x >> 6;
-  const long long env = (long long)blockIdx.x * MFG_WPB + wid;
+  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
   uint8_t* rec = state + (size_t)env * S->L.size;
   const int debt = ((const int*)(rec + S->L.o_hdr))[H_DEBT];
@@ -2313,10 +2346,10 @@ static void pcg64_seed(uint32_t entropy, uint64_t* st_hi, uint64_t* st_lo, uint6
 static int align_up(int x, int a) { return (x + a - 1) / a * a; }
 
 static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int dropmax, int destmax, int mmax,
-                        int kmax, int mstate_ints, int path_cap, int graph) {
+                        int kmax, int mstate_ints, int path_cap, int graph, int dirt_cap) {
   int o = 0;
   const int A = s->n_agents, nd = s->n_doors;
-  const int dm = s->has_dirt ? MFG_DIRT_MAX : 0;
+  const int dm = dirt_cap;
   L->o_hdr = o; o += 4 * MFG_HDR_N;
   L->o_rule_ctr = o; o += 4 * MFG_MAX_RULES;
   L->o_agent_pos = o; o += 4 * A;
@@ -2449,21 +2482,51 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   h.imax = imax; h.pmax = pmax; h.dropmax = dropmax; h.destmax = destmax; h.mmax = mmax; h.kmax = kmax;
   h.mstate_ints = MS_NEXT + mmax + 1;
   h.path_cap = moving ? std::min(std::min(4 * (s->H + s->W), s->n_floor), 1000) : 0;  // route fits the 2 KB scratch
-  make_layout(s, &h.L, imax, pmax, dropmax, destmax, mmax, kmax, h.mstate_ints, h.path_cap, moving);
+  // dirt-pile slots: the initial spawn plus every respawn one episode can hold (DoneAtMaxStepsReached bounds
+  // it; without it the engine's maximum). More piles than slots flag the env (H_OVERFLOW), never silently.
+  int dirt_q = 0;
+  h.dirt_cap = 0;
+  if (s->has_dirt) {
+    int max_steps = -1, respawn_n = 0, freq = 0;
+    for (int r = 0; r < s->n_rules; r++) {
+      if (s->rules[r].op == MFG_RULE_DONE_MAXSTEPS) max_steps = s->rules[r].i[0];
+      if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT) { freq = s->rules[r].i[0]; respawn_n = s->rules[r].i[1]; }
+    }
+    dirt_q = std::max(s->dirt_quantity, respawn_n);
+    long long need = (long long)s->dirt_quantity + 1;
+    if (respawn_n > 0) need = max_steps < 0 ? MFG_DIRT_MAX : need + (long long)(max_steps / (freq + 1) + 1) * (respawn_n + 1);
+    h.dirt_cap = (int)std::min<long long>(MFG_DIRT_MAX, std::max<long long>(MFG_WAVE, (need + 63) / 64 * 64));
+  }
+  // per-wave LDS scratch: spawn positions + amounts of the largest dirt spawn, maintainer routes, >= 2 KB
+  h.scratch_bytes = align_up(std::max({2048, 12 * (dirt_q + 2) + 16, 2 * (h.path_cap + 2)}), 16);
+  make_layout(s, &h.L, imax, pmax, dropmax, destmax, mmax, kmax, h.mstate_ints, h.path_cap, moving, h.dirt_cap);
   h.step_rng = 0;
   for (int r = 0; r < s->n_rules; r++)  // dirt spawns and maintainer retargets consume the floor order mid-step
     if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT || s->rules[r].op == MFG_RULE_MOVE_MAINTAINERS) h.step_rng = 1;
   h.map_bytes = align_up(2 * HW, 16);
   h.map_bytes8 = align_up(HW, 16);
-  h.lds_full = align_up(h.L.size + 2048 + 4 * MFG_STAB_N, 16);
-  // BFS scratch of the maintainer routing: pred, succ, two fringes, level copy (u16 each) + discovery keys
-  h.bfs_off = moving ? h.lds_full : 0;
-  if (moving) h.lds_full = align_up(h.lds_full + 10 * h.nf + 4 * h.nf + 64, 16);
+  h.lds_full = align_up(h.L.size + h.scratch_bytes + 4 * MFG_STAB_N, 16);
+  // BFS scratch of the maintainer routing: pred, succ, two fringes, level copy (u16 each) + discovery keys;
+  // in the LDS slice when it fits, else a per-env HBM pool (grid128: 212 KB per env)
+  h.bfs_bytes = moving ? align_up(10 * h.nf + 4 * h.nf + 64, 16) : 0;
+  h.bfs_off = 0;
+  h.bfs_pool = nullptr;
+  const char* force_hbm = getenv("MFG_BFS_HBM");  // test hook: the HBM pool path on small levels too
+  const bool bfs_lds = moving && h.lds_full + h.bfs_bytes <= MFG_LDS_MAX && !(force_hbm && force_hbm[0] == '1');
+  if (bfs_lds) {
+    h.bfs_off = h.lds_full;
+    h.lds_full = align_up(h.lds_full + h.bfs_bytes, 16);
+  }
+  // identifier-collision pairs of the obs dedupe: per int-id entity one wall and one door partner and at
+  // most one partner per other kind (identifiers are unique within a kind), plus the static Wall/Door pairs
+  {
+    const int tot_cap = imax + pmax + dropmax + destmax + h.dirt_cap + mmax + kmax;
+    h.max_pairs = std::max(16, 2 * tot_cap + 3 * tot_cap);
+  }
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
   h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
-  h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) + 12 * OBS_MAX_PAIRS +
-              4 * h.fv_words + align_up(h.dd, 16) +
-              4 * MFG_WAVE;
+  h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) + 12 * h.max_pairs +
+              4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + (h.dirt_cap > MFG_WAVE ? h.dirt_cap / 8 : 0);
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
@@ -2502,6 +2565,11 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
     }
   }
   h.n_wd_pairs = (int)(wd.size() / 3);
+  h.max_pairs += h.n_wd_pairs;
+  h.lds_obs += 12 * h.n_wd_pairs;
+  if (h.lds_full > MFG_LDS_MAX || h.lds_obs > MFG_LDS_MAX || h.lds_replay_per_wave > MFG_LDS_MAX) {
+    delete e; return fail("env record does not fit one CU's 160 KB of LDS");
+  }
   std::vector<int8_t> rp((size_t)h.nrays * h.maxpts * 2, 0);
   std::vector<uint8_t> rlen(h.nrays);
   for (int r = 0; r < h.nrays; r++) {
@@ -2534,6 +2602,17 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   if (hipMalloc((void**)&e->d_state, (size_t)h.L.size * (size_t)n_envs) != hipSuccess) {
     delete e; return fail("state allocation failed");
   }
+  if (h.bfs_bytes && !h.bfs_off) {  // BFS scratch in HBM, one slice per env
+    void* pool = nullptr;
+    if (hipMalloc(&pool, (size_t)h.bfs_bytes * (size_t)n_envs) != hipSuccess) {
+      delete e; return fail("BFS scratch allocation failed");
+    }
+    e->d_bufs.push_back(pool);
+    h.bfs_pool = (uint8_t*)pool;
+    if (hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
+      delete e; return fail("spec upload failed");
+    }
+  }
   e->maxpts = h.maxpts;
   *out = e;
   return 0;
@@ -2552,13 +2631,15 @@ extern "C" int mfg_destroy(mfg_engine* e) {
 }
 
 // record layout for host-side decoding (tests, snapshots):
-// [size, o_hdr, ..., o_perm, lmax, obs_agent_stride, lds_full, xchg_ordered]
+// [size, o_hdr, ..., o_perm, lmax, obs_agent_stride, lds_full, xchg_ordered, o_machines, ..., scratch_bytes]
 extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
   const MfgLayout& L = e->h.L;
   const int32_t v[] = {L.size, L.o_hdr, L.o_rule_ctr, L.o_agent_pos, L.o_agent_arr, L.o_agent_par, L.o_frozen_org,
                        L.o_frozen_gp, L.o_door, L.o_items, L.o_pods, L.o_drops, L.o_dests, L.o_dirt_pos,
                        L.o_dirt_id, L.o_battery, L.o_frozen_bat, L.o_dirt_amt, L.o_pcg, L.o_mt, L.o_perm,
-                       e->h.lmax, e->h.obs_agent_stride, e->h.lds_full, e->h.xchg_ordered};
+                       e->h.lmax, e->h.obs_agent_stride, e->h.lds_full, e->h.xchg_ordered, L.o_machines,
+                       L.o_maints, L.o_mstate, L.o_mpath, L.o_grank, e->h.dirt_cap, e->h.lds_logic, e->h.lds_obs,
+                       e->h.lds_replay_per_wave, e->h.bfs_off, e->h.bfs_bytes, e->h.max_pairs, e->h.scratch_bytes};
   const int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
@@ -2566,15 +2647,19 @@ extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
 
 extern "C" void* mfg_state_ptr(mfg_engine* e) { return e ? e->d_state : nullptr; }
 
-static unsigned env_grid(const mfg_engine* e) { return (unsigned)((e->B + MFG_WPB - 1) / MFG_WPB); }
+// waves per workgroup for a per-wave LDS slice: up to MFG_WPB, as many as one CU's LDS holds
+static int wpb_for(size_t lds) { return (int)std::max<size_t>(1, std::min<size_t>(MFG_WPB, MFG_LDS_MAX / std::max<size_t>(lds, 1))); }
+static unsigned env_grid(const mfg_engine* e, int wpb) { return (unsigned)((e->B + wpb - 1) / wpb); }
+// launch geometry of a kernel with `lds` bytes of dynamic LDS per wave
+#define GEOM(lds) dim3(env_grid(e, wpb_for(lds))), dim3(wpb_for(lds) * 64), (size_t)(lds) * wpb_for(lds)
 
 template <int MP, typename OT>
 static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
   if (e->h.mmax || e->h.kmax)
-    hipLaunchKernelGGL((k_obs<MP, OT, true>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_obs * MFG_WPB,
+    hipLaunchKernelGGL((k_obs<MP, OT, true>), GEOM(e->h.lds_obs),
                        st, e->d_spec, e->d_state, (long long)e->B, obs);
   else
-    hipLaunchKernelGGL((k_obs<MP, OT, false>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_obs * MFG_WPB,
+    hipLaunchKernelGGL((k_obs<MP, OT, false>), GEOM(e->h.lds_obs),
                        st, e->d_spec, e->d_state, (long long)e->B, obs);
   return hipGetLastError();
 }
@@ -2613,7 +2698,7 @@ extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_
   if (!e) return fail("null engine");
   hipStream_t st = (hipStream_t)stream;
   PROF_BEGIN(e, st);
-  hipLaunchKernelGGL(k_reset, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_full * MFG_WPB, st, e->d_spec,
+  hipLaunchKernelGGL(k_reset, GEOM(e->h.lds_full), st, e->d_spec,
                      e->d_state, (long long)e->B, mask, init, (unsigned long long)seed_base);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_reset launch: ") + hipGetErrorString(err));
@@ -2624,10 +2709,9 @@ extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_
 // Pay all pending floor-shuffle debt (membership-only shuffles of the reference's move checks, Q3).
 extern "C" int mfg_replay(mfg_engine* e, void* stream) {
   if (!e) return fail("null engine");
-  const size_t lds = (size_t)e->h.lds_replay_per_wave * MFG_WPB;
   hipStream_t st = (hipStream_t)stream;
   PROF_BEGIN(e, st);
-  hipLaunchKernelGGL(k_replay, dim3(env_grid(e)), dim3(MFG_WPB * 64), lds, st, e->d_spec, e->d_state,
+  hipLaunchKernelGGL(k_replay, GEOM(e->h.lds_replay_per_wave), st, e->d_spec, e->d_state,
                      (long long)e->B);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
@@ -2653,22 +2737,22 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
     const size_t kb = (size_t)k * B;
     {
     PROF_BEGIN(e, st);
-    if (e->h.bfs_off) {
-    hipLaunchKernelGGL((k_logic<true, true>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+    if (e->h.bfs_bytes) {
+    hipLaunchKernelGGL((k_logic<true, true>), GEOM(e->h.lds_logic), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
                        auto_reset);
     } else if (e->h.step_rng) {
-    hipLaunchKernelGGL((k_logic<true, false>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+    hipLaunchKernelGGL((k_logic<true, false>), GEOM(e->h.lds_logic), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
                        auto_reset);
     } else {
-    hipLaunchKernelGGL((k_logic<false, false>), dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_logic * MFG_WPB, st,
+    hipLaunchKernelGGL((k_logic<false, false>), GEOM(e->h.lds_logic), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
@@ -2681,7 +2765,7 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
     }
     if (auto_reset) {
       PROF_BEGIN(e, st);
-      hipLaunchKernelGGL(k_resetdone, dim3(env_grid(e)), dim3(MFG_WPB * 64), (size_t)e->h.lds_full * MFG_WPB, st,
+      hipLaunchKernelGGL(k_resetdone, GEOM(e->h.lds_full), st,
                          e->d_spec, e->d_state, (long long)e->B);
       hipError_t err = hipGetLastError();
       if (err != hipSuccess) return fail(std::string("k_resetdone launch: ") + hipGetErrorString(err));

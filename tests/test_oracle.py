@@ -11,7 +11,7 @@ import golden_compare as G
 UNITS = np.load(G.GOLDEN / 'units.npz')
 FIXTURES = [('large8', 'large8.yaml'), ('rooms4', 'rooms4.yaml'), ('simple1', 'simple1.yaml'),
             ('alltest16', 'alltest16.yaml'), ('default_large', 'default_large.yaml'),
-            ('maint_rooms', 'maint_rooms.yaml')]
+            ('maint_rooms', 'maint_rooms.yaml'), ('grid128_64', 'grid128_64.yaml')]
 
 
 def test_mt19937_matches_cpython():

@@ -216,6 +216,7 @@ def main():
     ap.add_argument('--steps', type=int, default=1200)
     ap.add_argument('--full-obs-every', type=int, default=97)
     ap.add_argument('--tag', default=None)
+    ap.add_argument('--level', default=None, help='custom level file name under mfg_amd/levels (C5: grid128.txt)')
     ap.add_argument('--units', action='store_true')
     args = ap.parse_args()
     outdir = REPO / 'tests' / 'golden'
@@ -224,7 +225,7 @@ def main():
         unit_vectors(outdir / 'units.npz')
         print('wrote units.npz')
         return
-    level_path = None
+    level_path = str(LVL_DIR / args.level) if args.level else None
     tag = args.tag or Path(args.config).stem
     for s in [int(x) for x in args.seeds.split(',')]:
         rec, obs_full, floors, keys = run(args.config, s, args.steps, 1000 + s, args.full_obs_every, level_path)
