@@ -38,9 +38,32 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "env-steps/sec (whole node), 8-agent 'large' level, batch 65536, 1/2/4/8 MI355X"
 
 
+def core_bytes(spec):
+    """SURVEY §8(d) canonical minimal SoA bytes per env-step without the obs: mutable state read + written
+    (agent pos u16, door open+timer u8, item/dirt positions u16, battery and dirt amounts f64, 7 B of
+    counters), per-episode constants read (pod/drop-off/destination/machine/maintainer positions, frozen
+    ray origins u16, frozen battery f64, entity ids i32), actions u8, reward f64, done u8. C3: 415 B."""
+    from mfg_amd import abi
+    c = spec.c
+    A = spec.n_agents
+    q = {int(r.op): r for r in c.rules[:c.n_rules]}
+
+    def spawn(op):
+        return int(q[op].i[0]) if op in q else 0
+    bat = 8 * A if abi.RULE_SPAWN_BATTERIES in q else 0
+    mut = 2 * A + c.n_doors + 2 * spawn(abi.RULE_SPAWN_ITEMS) + bat + 7
+    if c.has_dirt:
+        mut += 10 * int(c.dirt_quantity)
+    const = 2 * A + bat + 4 * A
+    for op in (abi.RULE_SPAWN_PODS, abi.RULE_SPAWN_DROPOFFS, abi.RULE_SPAWN_DESTS, abi.RULE_SPAWN_MACHINES,
+               abi.RULE_SPAWN_MAINTAINERS):
+        const += 2 * spawn(op)
+    return 2 * mut + const + A + 8 * A + 1
+
+
 def algo_bytes(kernel, spec, obs_bytes_per_env, k_launch):
     """Algorithmic (minimal) bytes one launch of `kernel` moves per env."""
-    core = 415 if spec.n_agents == 8 else None  # SURVEY §8(d) canonical SoA, C3
+    core = core_bytes(spec)
     if kernel == 'k_logic':
         return core
     if kernel == 'k_obs':
@@ -219,7 +242,8 @@ def main():
         traffic = None
         if pmc and dom and dom in pmc.get('hbm_bytes_per_launch', {}):
             traffic = pmc['hbm_bytes_per_launch'][dom]
-        pipe_bytes = ALGO_BYTES_PER_ENV_STEP * B * k_call
+        step_bytes = core_bytes(spec) + obs_bytes  # C3: 415 + 10,976 = ALGO_BYTES_PER_ENV_STEP
+        pipe_bytes = step_bytes * B * k_call
         if dom:
             dk = kernels[dom]
             achieved = dk["achieved_GBs"]
@@ -227,7 +251,7 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
                     "kernel": dom, "mean_launch_ms": dk["mean_launch_ms"],
                     "algo_bytes_per_launch": dk["algo_bytes_per_launch"],
-                    "pipeline": {"algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
+                    "pipeline": {"algo_bytes_per_env_step": step_bytes,
                                  "env_steps_per_call": B * k_call, "mean_call_ms": round(mean_call * 1e3, 3),
                                  "achieved": round(pipe_bytes / mean_call / 1e9, 2),
                                  "frac": round(pipe_bytes / mean_call / 1e9 / HBM_PEAK_GBS, 5)},

@@ -101,6 +101,12 @@ struct Env {
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// lanes exchange through HBM scratch (BFS pool, pair spill): workgroup-scope fence (s_waitcnt on LDS and
+// vector memory), then the wave barrier
+__device__ __forceinline__ void mem_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // ------------------------------------------------------------------------------------------------
 // MT19937 (CPython semantics) — state in LDS, lane-parallel twist
@@ -1680,6 +1686,13 @@ struct RayLane {
 // 5 drop, 6 dirt, 7 dest, 8 machine, 9 maintainer, 15 wall -> slot unused, the wall is identified by its
 // cell). The dynamic int-id entities are the concatenation items, pods, drops, dests, dirt, machines,
 // maintainers, handled 64 per pass. Returns the pair count (<= S->max_pairs, a bound from the group sizes).
+// the first pairs_lds pairs live in LDS, the rest (rare: many colliding identifiers) in the env's HBM pool
+struct PairList {
+  int* lds;
+  int* glob;
+  int nl;
+  __device__ __forceinline__ int* at(int q) const { return q < nl ? lds + 3 * q : glob + 3 * (q - nl); }
+};
 struct IdEnt {
   int kind, slot, cell, id;
 };
@@ -1701,7 +1714,7 @@ __device__ __forceinline__ IdEnt id_entity(const Env& e, int l, int nI, int nP, 
   return r;
 }
 template <bool MM>
-__device__ int build_id_pairs(const Env& e, int* pairs) {
+__device__ int build_id_pairs(const Env& e, const PairList& pairs) {
   SpecP S = e.S;
   const int lane = e.lane, cap = S->max_pairs;
   const int nI = e.H(H_N_ITEMS), nP = e.H(H_N_PODS), nR = e.H(H_N_DROPS), nS = e.H(H_N_DESTS), nT = e.H(H_N_DIRT);
@@ -1711,7 +1724,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
   auto emit = [&](bool has, int cA, int cB, int codes) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
-    if (has && rank < cap) { pairs[3 * rank] = cA; pairs[3 * rank + 1] = cB; pairs[3 * rank + 2] = codes; }
+    if (has && rank < cap) { int* p = pairs.at(rank); p[0] = cA; p[1] = cB; p[2] = codes; }
     n += popc(m);
   };
   for (int b = 0; b < tot; b += MFG_WAVE) {
@@ -1750,7 +1763,7 @@ __device__ int build_id_pairs(const Env& e, int* pairs) {
     emit(has, dc, wc, ((K_DOOR << 12) | k) | (K_WALL << 28));
   }
   if (n > cap) e.setH(H_OVERFLOW, 1);
-  wave_sync();
+  mem_sync();
   return n < cap ? n : cap;
 }
 
@@ -1787,22 +1800,24 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
 }
 
 template <int MAXPTS, typename OT, bool MM>
-__device__ void build_obs(const Env& e, OT* out_env) {
+__device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   SpecP S = e.S;
   const int A = S->A, H = S->s.H, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
   const int lane = e.lane;
   const bool frozen = e.H(H_FROZEN) != 0;
   build_cmap<MM>(e);
-  int* pairs = e.scratch;
+  const PairList pairs{e.scratch, pair_glob, S->pairs_lds};
   const int npairs = build_id_pairs<MM>(e, pairs);
   for (int q = lane; q < npairs; q += MFG_WAVE) {  // cells -> packed (x << 16 | y), agent independent
-    const int cA = pairs[3 * q], cB = pairs[3 * q + 1];
-    pairs[3 * q] = ((cA / W) << 16) | (cA % W);
-    pairs[3 * q + 1] = ((cB / W) << 16) | (cB % W);
+    int* p = pairs.at(q);
+    const int cA = p[0], cB = p[1];
+    p[0] = ((cA / W) << 16) | (cA % W);
+    p[1] = ((cB / W) << 16) | (cB % W);
   }
+  if (npairs > S->pairs_lds) mem_sync();
   // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
   // ray * 32 + point; it gives both the window visibility and the dedupe order (Q14)
-  uint32_t* fv = (uint32_t*)(e.scratch + 3 * S->max_pairs);
+  uint32_t* fv = (uint32_t*)(e.scratch + 3 * S->pairs_lds);
   const int fw = 2 * d + 1, fn = fw * fw;
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
@@ -1861,7 +1876,8 @@ __device__ void build_obs(const Env& e, OT* out_env) {
     sup.dsup = dsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
-      const int pA = q < npairs ? pairs[3 * q] : 0, pB = q < npairs ? pairs[3 * q + 1] : 0;
+      const int* pq = pairs.at(q < npairs ? q : 0);
+      const int pA = q < npairs ? pq[0] : 0, pB = q < npairs ? pq[1] : 0;
       const int xA = (pA >> 16) - ox + d, yA = (pA & 0xFFFF) - oy + d;
       const int xB = (pB >> 16) - ox + d, yB = (pB & 0xFFFF) - oy + d;
       const bool nearq = q < npairs && (unsigned)xA < (unsigned)fw && (unsigned)yA < (unsigned)fw &&
@@ -1872,7 +1888,7 @@ __device__ void build_obs(const Env& e, OT* out_env) {
         const int L = ffs64(hm);
         hm &= hm - 1;
         const int qq = q0 + L;
-        const int codes = pairs[3 * qq + 2];  // codeA | codeB << 16
+        const int codes = pairs.at(qq)[2];  // codeA | codeB << 16
         if (rl((int)rA, L) < rl((int)rB, L)) sup_add(sup, (codes >> 16) & 0xFFFF, rl(pB, L), lane);
         else sup_add(sup, codes & 0xFFFF, rl(pA, L), lane);
       }
@@ -2038,6 +2054,7 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
 //   k_obs       observation render; LDS = lean record + cell map + id-collision pairs; read-only on state
 // and k_replay pays the accumulated floor-shuffle debt once per mfg_step call.
 // ------------------------------------------------------------------------------------------------
+#define MFG_PAIRS_LDS 128    // identifier-collision pairs kept in the k_obs LDS slice
 #define MFG_LDS_MAX 163840  // LDS bytes per CU on gfx950 (one workgroup may use all of it)
 #define MFG_WPB 4  // waves (envs) per workgroup at most; fewer when a slice is large (wpb_for)
 
@@ -2200,7 +2217,8 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, cons
   const uint8_t* rec = state + (size_t)env * S->L.size;
   rec_copy(e.lds, rec, S->L.o_mt, e.lane);
   wave_sync();
-  build_obs<MAXPTS, OT, MM>(e, obs + (size_t)env * S->A * S->obs_agent_stride);
+  int* pg = S->pair_pool ? S->pair_pool + (size_t)env * 3 * (S->max_pairs - S->pairs_lds) : nullptr;
+  build_obs<MAXPTS, OT, MM>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg);
   if (e.lane == 0 && e.hdrp[H_OVERFLOW]) ((int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_OVERFLOW] = 1;
 }
 
@@ -2523,9 +2541,10 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
     const int tot_cap = imax + pmax + dropmax + destmax + h.dirt_cap + mmax + kmax;
     h.max_pairs = std::max(16, 2 * tot_cap + 3 * tot_cap);
   }
+  h.pair_pool = nullptr;
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
   h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
-  h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) + 12 * h.max_pairs +
+  h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + (h.dirt_cap > MFG_WAVE ? h.dirt_cap / 8 : 0);
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
@@ -2566,7 +2585,10 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   }
   h.n_wd_pairs = (int)(wd.size() / 3);
   h.max_pairs += h.n_wd_pairs;
-  h.lds_obs += 12 * h.n_wd_pairs;
+  // LDS holds up to MFG_PAIRS_LDS pairs (the usual case); the bound's remainder spills to an HBM pool
+  h.pairs_lds = std::min(h.max_pairs, MFG_PAIRS_LDS);
+  if (const char* f = getenv("MFG_PAIRS_LDS")) h.pairs_lds = std::max(1, std::min(h.pairs_lds, atoi(f)));  // test hook
+  h.lds_obs += 12 * h.pairs_lds;
   if (h.lds_full > MFG_LDS_MAX || h.lds_obs > MFG_LDS_MAX || h.lds_replay_per_wave > MFG_LDS_MAX) {
     delete e; return fail("env record does not fit one CU's 160 KB of LDS");
   }
@@ -2602,6 +2624,14 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   if (hipMalloc((void**)&e->d_state, (size_t)h.L.size * (size_t)n_envs) != hipSuccess) {
     delete e; return fail("state allocation failed");
   }
+  if (h.max_pairs > h.pairs_lds) {  // identifier-pair spill in HBM, one slice per env
+    void* pool = nullptr;
+    if (hipMalloc(&pool, (size_t)12 * (h.max_pairs - h.pairs_lds) * (size_t)n_envs) != hipSuccess) {
+      delete e; return fail("pair pool allocation failed");
+    }
+    e->d_bufs.push_back(pool);
+    h.pair_pool = (int*)pool;
+  }
   if (h.bfs_bytes && !h.bfs_off) {  // BFS scratch in HBM, one slice per env
     void* pool = nullptr;
     if (hipMalloc(&pool, (size_t)h.bfs_bytes * (size_t)n_envs) != hipSuccess) {
@@ -2609,9 +2639,10 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
     }
     e->d_bufs.push_back(pool);
     h.bfs_pool = (uint8_t*)pool;
-    if (hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
-      delete e; return fail("spec upload failed");
-    }
+  }
+  if ((h.bfs_pool || h.pair_pool) &&
+      hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
+    delete e; return fail("spec upload failed");
   }
   e->maxpts = h.maxpts;
   *out = e;
