@@ -115,16 +115,19 @@ __device__ __forceinline__ void mem_sync() {
 #define MT_LOWER 0x7fffffffu
 #define MT_MATRIX 0x9908b0dfu
 
+// v_bitop3_b32 (gfx950): LUT 0x78 = a ^ (b & c), 0xE4 = c ? a : b bitwise (a = 0xF0, b = 0xCC, c = 0xAA)
+#define XOR_AND(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x78)
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
+  y = XOR_AND(y, y << 7, 0x9d2c5680u);
+  y = XOR_AND(y, y << 15, 0xefc60000u);
   y ^= (y >> 18);
   return y;
 }
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
-  return c ^ (y >> 1) ^ ((y & 1u) ? MT_MATRIX : 0u);
+  const uint32_t y = __builtin_amdgcn_bitop3_b32(a, b, MT_UPPER, 0xE4);  // (a & UPPER) | (b & LOWER)
+  const uint32_t odd = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);       // y & 1 == b & 1, as a mask
+  return XOR_AND(c ^ (y >> 1), odd, MT_MATRIX);
 }
 // In-place twist in its three dependency phases (i<227: old inputs; 227<=i<454: mt[i-227] new;
 // 454<=i<623: mt[i-227] new). Each phase issues all its LDS reads before any of its writes, so one
@@ -216,7 +219,8 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
     }
     const int lmax = 624 - idx;
     const bool has = lane < lmax;
-    const uint32_t y = mt_temper(mt[has ? idx + lane : 623]);
+    // lanes past the state read the words after it (perm / scratch, inside the slice) and are discarded
+    const uint32_t y = mt_temper(mt[idx + lane]);
     int A;
     u64 accm;
     int il;
@@ -367,7 +371,7 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
       idx = 0;
     }
     const bool has = lane < 624 - idx;
-    const uint32_t y = mt_temper(mt[has ? idx + lane : 623]);
+    const uint32_t y = mt_temper(mt[idx + lane]);  // lanes past the state: discarded (slice-internal read)
     int A;
     uint32_t r;
     bool act, acc;
@@ -1687,11 +1691,22 @@ struct RayLane {
 // cell). The dynamic int-id entities are the concatenation items, pods, drops, dests, dirt, machines,
 // maintainers, handled 64 per pass. Returns the pair count (<= S->max_pairs, a bound from the group sizes).
 // the first pairs_lds pairs live in LDS, the rest (rare: many colliding identifiers) in the env's HBM pool
+// (explicit branches, not a pointer select, so LDS accesses stay ds_* instead of flat)
+typedef __attribute__((address_space(3))) int lds_int;
+typedef __attribute__((address_space(1))) int glb_int;
 struct PairList {
-  int* lds;
-  int* glob;
+  lds_int* lds;
+  glb_int* glob;
   int nl;
-  __device__ __forceinline__ int* at(int q) const { return q < nl ? lds + 3 * q : glob + 3 * (q - nl); }
+  __device__ __forceinline__ void put(int q, int a, int b, int c) const {
+    if (q < nl) { lds[3 * q] = a; lds[3 * q + 1] = b; lds[3 * q + 2] = c; }
+    else { glb_int* g = glob + 3 * (q - nl); g[0] = a; g[1] = b; g[2] = c; }
+  }
+  __device__ __forceinline__ int get(int q, int k) const { return q < nl ? lds[3 * q + k] : glob[3 * (q - nl) + k]; }
+  __device__ __forceinline__ void set(int q, int k, int v) const {
+    if (q < nl) lds[3 * q + k] = v;
+    else glob[3 * (q - nl) + k] = v;
+  }
 };
 struct IdEnt {
   int kind, slot, cell, id;
@@ -1724,7 +1739,7 @@ __device__ int build_id_pairs(const Env& e, const PairList& pairs) {
   auto emit = [&](bool has, int cA, int cB, int codes) {
     const u64 m = ballot(has);
     const int rank = n + mbcnt(m);
-    if (has && rank < cap) { int* p = pairs.at(rank); p[0] = cA; p[1] = cB; p[2] = codes; }
+    if (has && rank < cap) pairs.put(rank, cA, cB, codes);
     n += popc(m);
   };
   for (int b = 0; b < tot; b += MFG_WAVE) {
@@ -1768,12 +1783,12 @@ __device__ int build_id_pairs(const Env& e, const PairList& pairs) {
 }
 
 struct Sup {  // per-agent suppression sets from the identifier dedupe
-  u64 items, pods, drops, dests, dirt, doors, machines, maints;
+  u64 items, pods, drops, dests, doors, machines, maints;
   uint8_t* wsup;   // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
-  uint32_t* dsup;  // dirt slots >= 64: LDS bitmap [dirt_cap / 32] (null when dirt_cap <= 64)
+  __attribute__((address_space(3))) uint32_t* dsup;  // dirt slots: LDS bitmap [dirt_cap / 32]
   int ax, ay, r, d, W;
   __device__ __forceinline__ bool dirt_sup(int i) const {
-    return dsup ? ((dsup[i >> 5] >> (i & 31)) & 1u) != 0 : ((dirt >> (i & 63)) & 1ull) != 0;
+    return ((dsup[i >> 5] >> (i & 31)) & 1u) != 0;
   }
 };
 __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
@@ -1785,8 +1800,7 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
     case K_DROP: s.drops |= bit; break;
     case K_DEST: s.dests |= bit; break;
     case K_DIRT:
-      if (s.dsup) { if (lane == 0) s.dsup[slot >> 5] |= 1u << (slot & 31); }
-      else s.dirt |= bit;
+      if (lane == 0) s.dsup[slot >> 5] |= 1u << (slot & 31);
       break;
     case K_DOOR: s.doors |= bit; break;
     case K_MACHINE: s.machines |= bit; break;
@@ -1806,13 +1820,12 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   const int lane = e.lane;
   const bool frozen = e.H(H_FROZEN) != 0;
   build_cmap<MM>(e);
-  const PairList pairs{e.scratch, pair_glob, S->pairs_lds};
+  const PairList pairs{(lds_int*)e.scratch, (glb_int*)pair_glob, S->pairs_lds};
   const int npairs = build_id_pairs<MM>(e, pairs);
   for (int q = lane; q < npairs; q += MFG_WAVE) {  // cells -> packed (x << 16 | y), agent independent
-    int* p = pairs.at(q);
-    const int cA = p[0], cB = p[1];
-    p[0] = ((cA / W) << 16) | (cA % W);
-    p[1] = ((cB / W) << 16) | (cB % W);
+    const int cA = pairs.get(q, 0), cB = pairs.get(q, 1);
+    pairs.set(q, 0, ((cA / W) << 16) | (cA % W));
+    pairs.set(q, 1, ((cB / W) << 16) | (cB % W));
   }
   if (npairs > S->pairs_lds) mem_sync();
   // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
@@ -1822,7 +1835,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
   // dirt suppression bitmap for groups wider than a wave: after the per-lane sink words of the ray walk
-  uint32_t* dsup = S->dirt_cap > MFG_WAVE ? (uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE : nullptr;
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  lds_u32* dsup = (lds_u32*)((uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE);
   const int ndsup = S->dirt_cap >> 5;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
   const int agp = lane < A ? e.agpos()[lane] : -1;
@@ -1836,8 +1850,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
     const int ox = org / W, oy = org % W;
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
-    if (dsup)
-      for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
+    for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
     wave_sync();
     // ---- ray walk (lane = ray, 64 rays per pass): blocking bits first, then the walk on bitmasks ----
     for (int pass = 0; pass < npass; pass++) {
@@ -1870,14 +1883,13 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
     wave_sync();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     Sup sup;
-    sup.items = sup.pods = sup.drops = sup.dests = sup.dirt = sup.doors = sup.machines = sup.maints = 0;
+    sup.items = sup.pods = sup.drops = sup.dests = sup.doors = sup.machines = sup.maints = 0;
     sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
     sup.wsup = wsup;
     sup.dsup = dsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
-      const int* pq = pairs.at(q < npairs ? q : 0);
-      const int pA = q < npairs ? pq[0] : 0, pB = q < npairs ? pq[1] : 0;
+      const int pA = q < npairs ? pairs.get(q, 0) : 0, pB = q < npairs ? pairs.get(q, 1) : 0;
       const int xA = (pA >> 16) - ox + d, yA = (pA & 0xFFFF) - oy + d;
       const int xB = (pB >> 16) - ox + d, yB = (pB & 0xFFFF) - oy + d;
       const bool nearq = q < npairs && (unsigned)xA < (unsigned)fw && (unsigned)yA < (unsigned)fw &&
@@ -1888,7 +1900,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
         const int L = ffs64(hm);
         hm &= hm - 1;
         const int qq = q0 + L;
-        const int codes = pairs.at(qq)[2];  // codeA | codeB << 16
+        const int codes = pairs.get(qq, 2);  // codeA | codeB << 16
         if (rl((int)rA, L) < rl((int)rB, L)) sup_add(sup, (codes >> 16) & 0xFFFF, rl(pB, L), lane);
         else sup_add(sup, codes & 0xFFFF, rl(pA, L), lane);
       }
@@ -2545,7 +2557,7 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
   h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
-              4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + (h.dirt_cap > MFG_WAVE ? h.dirt_cap / 8 : 0);
+              4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8;
   // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
