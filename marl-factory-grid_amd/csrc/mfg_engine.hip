@@ -350,10 +350,13 @@ __device__ __forceinline__ uint32_t lds_xchg_u16(uint16_t* p, uint32_t v) {
 
 // k_replay's shuffle: the exchange path of mt_randbelow_seq specialised for the replay kernel (64
 // draws per chunk, the record's own u16 permutation, 16-bit exchanges). Out-of-play lanes read and write a per-lane sink word instead of
-// branching, so a block runs without exec-mask changes. stab: [64] rank table (tag << 6 | lane),
-// [64] chunk counter.
+// branching, so a block runs without exec-mask changes.
+// stab: [64] rank table (tag << 6 | lane), [64] chunk counter
 #define RP_CTR 64
 #define RP_STAB_N 68
+#ifndef RP_SERIAL_FWD
+#define RP_SERIAL_FWD 2  // blocks with at most this many forwards resolve them serially (no LDS table)
+#endif
 __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
@@ -372,56 +375,62 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     }
     const bool has = lane < 624 - idx;
     const uint32_t y = mt_temper(mt[idx + lane]);  // lanes past the state: discarded (slice-internal read)
-    int A;
-    uint32_t r;
-    bool act, acc;
-    u64 m;
-    if (icur - 63 >= lo && __clz(icur + 1) == __clz(icur - 62)) {
-      // fast path: i >= lo and bitlen(i+1) constant over the chunk -> accept <=> A <= c = icur - r
-      r = y >> __clz(icur + 1);
-      const int c = has ? icur - (int)r : -1;
-      A = mbcnt(ballot(c >= 63));
-      for (;;) {
-        m = ballot(A <= c);
-        const int n = mbcnt(m);
-        if (!ballot(n != A)) break;
-        A = n;
-      }
-      acc = A <= c;
-      act = has;
-    } else {
-      A = lane;
-      for (;;) {
-        const int il = icur - A;
-        act = has && il >= lo;
-        r = act ? y >> __clz(il + 1) : 0u;
-        acc = act && r <= (uint32_t)il;
-        m = ballot(acc);
-        const int n = mbcnt(m);
-        if (!ballot(n != A)) break;
-        A = n;
-      }
+    // One bit width per chunk: k = bitlen(icur + 1), and the chunk stops where bitlen(i + 1) would
+    // change (i < 2^(k-1) - 1) or at lo. Within it accept <=> A <= c = min(icur - r, span), with
+    // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
+    // start the next chunk). So every chunk takes the same branch-free path, power-of-two crossings
+    // and the i < 64 tail included.
+    const int sh = __clz(icur + 1);
+    const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank this chunk may take
+    const uint32_t r = y >> sh;
+    const int c = has ? min(icur - (int)r, span) : -1;
+    // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
+    u64 m = ballot(c >= 63);
+#ifdef MFG_ABLATE_NOJACOBI
+    m = ballot(mbcnt(ballot(c >= 0)) <= c);
+    if (0)
+#endif
+    for (;;) {
+      const u64 m2 = ballot(mbcnt(m) <= c);
+      if (m2 == m) break;
+      m = m2;
     }
-    const int consumed = popc(ballot(act));
+    const int A = mbcnt(m);
+    const bool acc = (m >> lane) & 1;
+    const int consumed = popc(ballot(has && A <= span));
     const int nacc = popc(m);
 #ifndef MFG_ABLATE_NOSWAP
     if (nacc) {
       const int imin = icur - nacc + 1;
       const int i = icur - A, j = (int)r;
       uint16_t* pi = acc ? &perm[i] : (uint16_t*)sink;
-      const int P0 = (int)*pi;
-      ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
-      const uint32_t tag = ctr << 6;
-      // pi: last earlier draw whose j is this draw's i (rank table keyed by icur - j; self-swaps excluded)
-      atomicMax(acc && j >= imin && j != i ? &ptab[icur - j] : sink, tag | (uint32_t)lane);
-      wave_sync();
-      const uint32_t tp = ptab[A & 63];
-      int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
-      int v = P0;
-      while (ballot(ptr >= 0)) {
-        const int src = ptr >= 0 ? ptr : lane;
-        const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
-        if (ptr >= 0) { v = v2; ptr = p2; }
+      int v = (int)*pi;
+      // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
+      // the block's own i range), the last one's V_s. Few forwards (large i): walk them in ascending s,
+      // so V_s is final before it is forwarded to rank icur - j_s (rejected lanes sharing that rank
+      // carry no swap and may take the value harmlessly). Many (small i): a rank table (tag | lane,
+      // keyed by icur - j) gives each draw its forward source and pointer jumping resolves the chains.
+      u64 cm = ballot(acc && j >= imin && j < i);
+      if (popc(cm) <= RP_SERIAL_FWD) {
+        while (cm) {
+          const int s = ffs64(cm);
+          cm &= cm - 1;
+          const int key = icur - rl(j, s);
+          const int vs = rl(v, s);
+          v = A == key ? vs : v;
+        }
+      } else {
+        ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
+        const uint32_t tag = ctr << 6;
+        atomicMax(acc && j >= imin && j < i ? &ptab[icur - j] : sink, tag | (uint32_t)lane);
+        wave_sync();
+        const uint32_t tp = ptab[A & 63];
+        int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
+        while (ballot(ptr >= 0)) {
+          const int src = ptr >= 0 ? ptr : lane;
+          const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
+          if (ptr >= 0) { v = v2; ptr = p2; }
+        }
       }
       // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j]
       const uint32_t F = lds_xchg_u16(acc ? &perm[j] : (uint16_t*)sink, (uint32_t)v);
