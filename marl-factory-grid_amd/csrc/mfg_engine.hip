@@ -33,6 +33,8 @@ __device__ __forceinline__ u64 lt_mask() { return (1ull << lane_id()) - 1ull; }
 __device__ __forceinline__ int mbcnt(u64 m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
+// a wave mask (SGPR pair) as a per-lane predicate, free (the mask is used as the condition directly)
+__device__ __forceinline__ bool lanes(u64 m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -347,6 +349,22 @@ __device__ __forceinline__ uint32_t lds_xchg_u16(uint16_t* p, uint32_t v) {
                : "memory");
   return (old >> sh) & 0xFFFFu;
 }
+// The same exchange split in two: issue (returns the raw old dword, not yet waited for), then wait
+// (tied to that value, so nothing reads it early) and extract the 16-bit half. LDS operations complete
+// in issue order, so the compiler's own counted lgkmcnt waits stay conservative around it.
+__device__ __forceinline__ uint32_t lds_xchg_u16_issue(uint16_t* p, uint32_t v) {
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  const uint32_t sh = (a & 2u) << 3;
+  const uint32_t mask = 0xFFFFu << sh, data = (v & 0xFFFFu) << sh;
+  uint32_t old;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(old) : "v"(a & ~3u), "v"(mask), "v"(data) : "memory");
+  return old;
+}
+__device__ __forceinline__ uint32_t lds_xchg_u16_wait(uint32_t old, uint16_t* p) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(old) : : "memory");
+  const uint32_t sh = ((uint32_t)(uintptr_t)p & 2u) << 3;
+  return (old >> sh) & 0xFFFFu;
+}
 
 // k_replay's shuffle: the exchange path of mt_randbelow_seq specialised for the replay kernel (64
 // draws per chunk, the record's own u16 permutation, 16-bit exchanges). Out-of-play lanes read and write a per-lane sink word instead of
@@ -366,15 +384,20 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
   int idx = e.H(H_MT_IDX);
   int icur = e.S->nf - 1;
   uint32_t ctr = (uint32_t)uni((int)e.stab[RP_CTR]);
+  // raw MT words of the next chunk, loaded one chunk ahead (lanes past the state read the words after
+  // it, inside the slice, and are discarded)
+  uint32_t yw = mt[min(idx, 624) + lane];
   while (icur >= lo) {
     if (idx >= 624) {
 #ifndef MFG_ABLATE_NOTWIST
       mt_twist(e);
 #endif
       idx = 0;
+      yw = mt[lane];
     }
     const bool has = lane < 624 - idx;
-    const uint32_t y = mt_temper(mt[idx + lane]);  // lanes past the state: discarded (slice-internal read)
+    const u64 hasm = ballot(has);
+    const uint32_t y = mt_temper(yw);
     // One bit width per chunk: k = bitlen(icur + 1), and the chunk stops where bitlen(i + 1) would
     // change (i < 2^(k-1) - 1) or at lo. Within it accept <=> A <= c = min(icur - r, span), with
     // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
@@ -396,22 +419,27 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
       m = m2;
     }
     const int A = mbcnt(m);
-    const bool acc = (m >> lane) & 1;
-    const int consumed = popc(ballot(has && A <= span));
+    const int consumed = popc(ballot(A <= span) & hasm);
     const int nacc = popc(m);
+    const int inext = icur - nacc, idxn = idx + consumed;
 #ifndef MFG_ABLATE_NOSWAP
     if (nacc) {
-      const int imin = icur - nacc + 1;
+      const bool acc = lanes(m);
       const int i = icur - A, j = (int)r;
       uint16_t* pi = acc ? &perm[i] : (uint16_t*)sink;
       int v = (int)*pi;
       // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
-      // the block's own i range), the last one's V_s. Few forwards (large i): walk them in ascending s,
-      // so V_s is final before it is forwarded to rank icur - j_s (rejected lanes sharing that rank
-      // carry no swap and may take the value harmlessly). Many (small i): a rank table (tag | lane,
-      // keyed by icur - j) gives each draw its forward source and pointer jumping resolves the chains.
-      u64 cm = ballot(acc && j >= imin && j < i);
-      if (popc(cm) <= RP_SERIAL_FWD) {
+      // the block's own i range [inext + 1, i)), the last one's V_s. Few forwards (large i): walk them
+      // in ascending s, so V_s is final before it is forwarded to rank icur - j_s (rejected lanes
+      // sharing that rank carry no swap and may take the value harmlessly). Many (small i): a rank
+      // table (tag | lane, keyed by icur - j) gives each draw its forward source and pointer jumping
+      // resolves the chains.
+      u64 cm = ballot(acc && j > inext && j < i);
+      const bool fwd = lanes(cm);
+      u64 cx = cm;  // clear the RP_SERIAL_FWD lowest forwards: none left <=> few enough (scalar ops only)
+#pragma unroll
+      for (int q = 0; q < RP_SERIAL_FWD; q++) cx &= cx - 1;
+      if (cx == 0) {
         while (cm) {
           const int s = ffs64(cm);
           cm &= cm - 1;
@@ -422,7 +450,7 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
       } else {
         ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
         const uint32_t tag = ctr << 6;
-        atomicMax(acc && j >= imin && j < i ? &ptab[icur - j] : sink, tag | (uint32_t)lane);
+        atomicMax(fwd ? &ptab[icur - j] : sink, tag | (uint32_t)lane);
         wave_sync();
         const uint32_t tp = ptab[A & 63];
         int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
@@ -432,15 +460,21 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
           if (ptr >= 0) { v = v2; ptr = p2; }
         }
       }
-      // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j]
-      const uint32_t F = lds_xchg_u16(acc ? &perm[j] : (uint16_t*)sink, (uint32_t)v);
-      wave_sync();
+      // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
+      // The next chunk's MT words are loaded while the exchange is in flight.
+      uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : (uint16_t*)sink, (uint32_t)v);
+      yw = mt[min(idxn, 624) + lane];
+      F = lds_xchg_u16_wait(F, acc ? &perm[j] : (uint16_t*)sink);
       *pi = (uint16_t)F;
       wave_sync();
+    } else {
+      yw = mt[min(idxn, 624) + lane];
     }
+#else
+    yw = mt[min(idxn, 624) + lane];
 #endif
-    icur -= nacc;
-    idx += consumed;
+    icur = inext;
+    idx = idxn;
   }
   if (lane == 0) e.stab[RP_CTR] = ctr;
   e.setH(H_MT_IDX, idx);
