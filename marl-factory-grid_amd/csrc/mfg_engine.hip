@@ -137,9 +137,9 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
 __device__ void mt_twist(const Env& e) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
-  // lanes outside a phase store into their own scratch word instead of branching (no exec-mask
-  // juggling); every kernel that owns MT state has a scratch area
-  uint32_t* sink = (uint32_t*)e.scratch + lane;
+  // lanes outside a phase store into a scratch word instead of branching (no exec-mask juggling);
+  // every kernel that owns MT state has >= 128 B of scratch (two lanes share a sink word)
+  uint32_t* sink = (uint32_t*)e.scratch + (lane >> 1);
   uint32_t v[4];
 #pragma unroll
   for (int t = 0; t < 4; t++) {
@@ -371,14 +371,16 @@ __device__ __forceinline__ uint32_t lds_xchg_u16_wait(uint32_t old, uint16_t* p)
 // branching, so a block runs without exec-mask changes.
 // stab: [64] rank table (tag << 6 | lane), [64] chunk counter
 #define RP_CTR 64
-#define RP_STAB_N 68
+#define RP_STAB_N 65
+#define RP_HDR_N 8  // header ints k_replay keeps in its slice (H_DEBT, H_MT_IDX)
+static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice");
 #ifndef RP_SERIAL_FWD
 #define RP_SERIAL_FWD 2  // blocks with at most this many forwards resolve them serially (no LDS table)
 #endif
 __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
-  uint32_t* sink = (uint32_t*)e.scratch + lane;
+  uint16_t* sink = (uint16_t*)e.scratch + lane;  // 128 B: one u16 per lane
   uint32_t* ptab = e.stab;
   const int lo = 1;
   int idx = e.H(H_MT_IDX);
@@ -426,7 +428,7 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     if (nacc) {
       const bool acc = lanes(m);
       const int i = icur - A, j = (int)r;
-      uint16_t* pi = acc ? &perm[i] : (uint16_t*)sink;
+      uint16_t* pi = acc ? &perm[i] : sink;
       int v = (int)*pi;
       // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
       // the block's own i range [inext + 1, i)), the last one's V_s. Few forwards (large i): walk them
@@ -450,7 +452,7 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
       } else {
         ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
         const uint32_t tag = ctr << 6;
-        atomicMax(fwd ? &ptab[icur - j] : sink, tag | (uint32_t)lane);
+        atomicMax(&ptab[fwd ? icur - j : lane], fwd ? tag | (uint32_t)lane : 0u);  // max with 0: no-op
         wave_sync();
         const uint32_t tp = ptab[A & 63];
         int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
@@ -462,9 +464,9 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
       }
       // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
       // The next chunk's MT words are loaded while the exchange is in flight.
-      uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : (uint16_t*)sink, (uint32_t)v);
+      uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
       yw = mt[min(idxn, 624) + lane];
-      F = lds_xchg_u16_wait(F, acc ? &perm[j] : (uint16_t*)sink);
+      F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
       *pi = (uint16_t)F;
       wave_sync();
     } else {
@@ -2291,7 +2293,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   // LDS slice laid out like the record prefix so Env accessors work: [hdr .. o_mt .. o_perm end]
   Env e;
   e.S = S;
-  e.lds = smem + (size_t)wid * S->lds_replay_per_wave - S->L.o_mt + 4 * MFG_HDR_N;
+  e.lds = smem + (size_t)wid * S->lds_replay_per_wave - S->L.o_mt + 4 * RP_HDR_N;
   e.lane = lane_id();
   e.scratch = (int*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_sink_off);
   e.cmap = nullptr;
@@ -2299,7 +2301,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   e.hdrp = (int*)(smem + (size_t)wid * S->lds_replay_per_wave);
   int* hdr = e.hdr();
   const int n16 = S->replay_mtperm >> 4;  // MT + u16 perm image of the record, 16 B units
-  if (e.lane < MFG_HDR_N) hdr[e.lane] = ((const int*)(rec + S->L.o_hdr))[e.lane];
+  if (e.lane < RP_HDR_N) hdr[e.lane] = ((const int*)(rec + S->L.o_hdr))[e.lane];
   {
     const uint4* src = (const uint4*)(rec + S->L.o_mt);
     uint4* dst = (uint4*)(e.lds + S->L.o_mt);
@@ -2601,12 +2603,12 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8;
-  // replay kernel slice: [hdr 128 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
+  // replay kernel slice: [hdr 32 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
     h.replay_mtperm = align_up(4 * 624 + 2 * h.nf, 16);  // o_perm == o_mt + 2496 (make_layout)
-    h.replay_sink_off = 4 * MFG_HDR_N + h.replay_mtperm;
-    h.replay_stab_off = h.replay_sink_off + 4 * MFG_WAVE;
+    h.replay_sink_off = 4 * RP_HDR_N + h.replay_mtperm;
+    h.replay_stab_off = h.replay_sink_off + 2 * MFG_WAVE;  // u16 sinks (replay_shuffle, mt_twist)
     h.replay_stab_n = h.xchg_ordered ? RP_STAB_N : MFG_STAB_N;
     h.lds_replay_per_wave = align_up(h.replay_stab_off + 4 * h.replay_stab_n, 16);
   }
