@@ -1866,7 +1866,11 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   const bool frozen = e.H(H_FROZEN) != 0;
   build_cmap<MM>(e);
   const PairList pairs{(lds_int*)e.scratch, (glb_int*)pair_glob, S->pairs_lds};
+#ifdef MFG_ABLATE_OB_NODEDUP
+  const int npairs = 0;
+#else
   const int npairs = build_id_pairs<MM>(e, pairs);
+#endif
   for (int q = lane; q < npairs; q += MFG_WAVE) {  // cells -> packed (x << 16 | y), agent independent
     const int cA = pairs.get(q, 0), cB = pairs.get(q, 1);
     pairs.set(q, 0, ((cA / W) << 16) | (cA % W));
@@ -1898,6 +1902,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
     wave_sync();
     // ---- ray walk (lane = ray, 64 rays per pass): blocking bits first, then the walk on bitmasks ----
+#ifdef MFG_ABLATE_OB_NORAY
+    for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0u;
+    if (0)
+#endif
     for (int pass = 0; pass < npass; pass++) {
       const int ray_id = pass * MFG_WAVE + lane;
       RayLane<MAXPTS> ray;
@@ -1954,6 +1962,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
     OT* out_a = out_env + (size_t)a * S->obs_agent_stride;
     const int nl = S->s.n_layers[a];
     // ---- placement (lane = window cell, 64 cells per pass): tag bits from the cell map ----
+#ifdef MFG_ABLATE_OB_NOPLACE
+    if (0)
+#endif
     for (int w0 = 0; w0 < dd; w0 += MFG_WAVE) {
       const int wi = w0 + lane;
       const bool inwin = wi < dd;
@@ -2001,7 +2012,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
         tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
       }
       u64 amask = 0;
+#ifndef MFG_ABLATE_OB_NOAMASK
       for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
+#endif
       // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
       // 0.4444 open, dirt = amount)
       auto tagv = [&](int tag) -> double {
