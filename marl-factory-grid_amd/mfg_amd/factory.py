@@ -22,6 +22,7 @@ from . import abi
 from .engine import Engine, RecordView, events_from_rows, EV_MISC, HDR, HDR_N
 from .info import rebuild_info
 from .spec import compile_spec, UnsupportedSpec
+from . import views as _views
 
 INIT_CREATE, INIT_KEEP_MT, INIT_NO_RESET = 1, 2, 4  # include/mfg.h MFG_INIT_*
 
@@ -83,6 +84,9 @@ class Factory:
         self._ev_m = torch.zeros((1, EV_MISC), dtype=torch.int32, device=self._dev)
         self._act = torch.zeros((1, A), dtype=torch.int32, device=self._dev)
         self._step = 0
+        self._agent_states = None  # agent.state per agent after the last step (None: all Noop/valid)
+        self._manual = None        # manual_* protocol: actions collected since manual_step_init
+        self._last = None          # (reward, done, info) of the last executed step
         # Factory.__init__: entities, rules, OBSBuilder (its floor-list access shuffles once, Q3)
         if self._sync:
             self._push_random()
@@ -150,6 +154,8 @@ class Factory:
         if self._sync:
             self._pull_random()
         self._torch.cuda.synchronize(self._dev)
+        self._agent_states = None
+        self._step = 0
         return {f'Agent[{n}]': o for n, o in zip(self.spec.agent_names, self._obs_list())}
 
     def step(self, actions):
@@ -169,17 +175,101 @@ class Factory:
                        ev_watch=self._ev_w, ev_misc=self._ev_m, auto_reset=False)
         if self._sync:
             self._pull_random()
-        ev = events_from_rows(self._ev_a[0].cpu().numpy(), self._ev_w[0].cpu().numpy(), self._ev_m[0].cpu().numpy())
+        ev_a, ev_w = self._ev_a[0].cpu().numpy(), self._ev_w[0].cpu().numpy()
+        ev = events_from_rows(ev_a, ev_w, self._ev_m[0].cpu().numpy())
         if ev['crashed']:
             raise RuntimeError('the reference crashes on this step (SURVEY App. A Q9/Q17); env state is flagged')
         reward = [float(x) for x in self._rew[0].cpu().numpy()]
         info = dict(rebuild_info(self.spec, [int(x) for x in actions], ev, reward))
         done = bool(self._done.item())
         self._step = ev['step']
+        self._agent_states = _views.agent_states(self.spec, actions, ev_a, ev_w)
+        self._last = (reward, done, info)
         return None, self._obs_list(), reward, done, info
 
+    # ---- entity views (factory.py:131-132, 262-292) ----
+    def snapshot(self):
+        """The env's state as a `views.Snapshot` (one device->host copy of the record)."""
+        return _views.snapshot_from_record(self._view(), self._agent_states)
+
+    def __getitem__(self, item):
+        """`env['Doors']` etc.: a read-only `views.GroupView` of the collection (factory.py:131-132)."""
+        return _views.group_view(self.spec, self.snapshot(), item)
+
+    def summarize_state(self):
+        return _views.summarize_state(self.spec, self.snapshot())
+
     def summarize_header(self):
-        return {'rec_step': self._step}
+        return _views.summarize_header(self.spec, self.snapshot())
+
+    def render(self, mode='human'):
+        """factory.py:262-273. The reference draws `state.entities.render()` with pygame; here 'human' prints
+        a text frame, 'ansi' returns it, 'entities' returns the RenderEntity list and 'rgb_array' an
+        (H, W, 3) uint8 image of it."""
+        snap = self.snapshot()
+        if mode == 'entities':
+            return _views.render_entities(self.spec, snap)
+        if mode == 'rgb_array':
+            return _views.render_rgb(self.spec, snap)
+        frame = _views.render_ansi(self.spec, snap)
+        if mode == 'ansi':
+            return frame
+        print(frame)
+        return None
+
+    def save_params(self, filepath):
+        """factory.py:294-298: copy the config file."""
+        import shutil
+        from pathlib import Path
+        filepath = Path(filepath)
+        filepath.parent.mkdir(parents=True, exist_ok=True)
+        shutil.copyfile(self.spec.config_path, filepath)
+
+    # ---- manual stepping (factory.py:150-187) ----
+    # The engine runs a whole step (pre-step rules, every agent in list order, step/post-step rules) in one
+    # device pass, so the manual protocol collects the agents' actions and executes the step at
+    # manual_finalize_init. Agents must be ticked once each, in list order; an agent's ActionResult is
+    # available after manual_finalize_init (ManualResult.resolve).
+    def manual_step_init(self):
+        self._manual = []
+        return []
+
+    def manual_agent_tick(self, agent_name, action):
+        if self._manual is None:
+            raise RuntimeError('manual_agent_tick before manual_step_init')
+        names = [f'Agent[{n}]' for n in self.spec.agent_names]
+        key = agent_name if agent_name in names else f'Agent[{agent_name}]'
+        if key not in names:
+            raise KeyError(f'"{agent_name}" could not be found. Check the spelling!')
+        a = names.index(key)
+        if a != len(self._manual):
+            raise RuntimeError('the engine executes agents in list order: tick each agent once, in order '
+                               f'(expected {names[len(self._manual)]}, got {key})')
+        if not 0 <= int(action) < self.spec.n_actions[a]:
+            raise IndexError(f'action {action} out of range for {key}')
+        self._manual.append(int(action))
+        return ManualResult(self, a)
+
+    def manual_finalize_init(self):
+        if self._manual is None or len(self._manual) != self.spec.n_agents:
+            raise RuntimeError('manual_finalize_init needs one manual_agent_tick per agent')
+        acts, self._manual = self._manual, None
+        self.step(acts)
+        return []
+
+    def manual_step_finalize(self, tick_result=None):
+        if self._last is None:
+            raise RuntimeError('no step has been executed')
+        return self._last
+
+    def manual_get_named_agent_obs(self, agent_name):
+        names = [f'Agent[{n}]' for n in self.spec.agent_names]
+        key = agent_name if agent_name in names else f'Agent[{agent_name}]'
+        a = names.index(key)
+        return list(self.spec.layer_names[a]), self._obs_list()[a]
+
+    def manual_get_agent_obs(self, agent_name):
+        return self.manual_get_named_agent_obs(agent_name)[1]
 
     def close(self):
         if getattr(self, '_eng', None) is not None:
@@ -191,6 +281,27 @@ class Factory:
 
     def __exit__(self, *a):
         self.close()
+
+
+class ManualResult:
+    """An agent's action result in the manual protocol, filled in once the step has executed."""
+
+    def __init__(self, env, agent):
+        self._env, self._a = env, agent
+
+    def resolve(self):
+        st = self._env._agent_states
+        if st is None:
+            raise RuntimeError('the step has not been executed yet (call manual_finalize_init)')
+        return st[self._a]
+
+    @property
+    def identifier(self):
+        return self.resolve()[0]
+
+    @property
+    def validity(self):
+        return self.resolve()[1]
 
 
 class BatchedFactory:

@@ -110,3 +110,59 @@ def test_batched_factory_matches_oracle():
             info = bf.info(0, acts[0])
             assert info['step'] == t + 1
     bf.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('tag', ['simple1', 'rooms4', 'large8', 'alltest16', 'default_large'])
+def test_facade_views_match_reference(tag):
+    """summarize_state / summarize_header / render entities of the facade (engine record -> views) equal
+    the reference's on the recorded actions, across episode resets (tools/gen_golden_views.py)."""
+    if not gpu_available():
+        pytest.skip('no GPU')
+    import views_compare as V
+    from mfg_amd.factory import Factory
+    rec = V.load_views(tag)
+    random.seed(rec['py_seed'])
+    env = Factory(rec['config'])
+    env.reset()
+    steps = rec['steps']
+    V.compare_record(env.spec, env.snapshot(), steps[0], f'{tag} reset')
+    assert env.summarize_state() == V.summarize_state(env.spec, env.snapshot())
+    for t, r in enumerate(steps[1:], 1):
+        if r['actions'] is None:
+            env.reset()
+        else:
+            env.step(r['actions'])
+        V.compare_record(env.spec, env.snapshot(), V.expand(r, steps[0]), f'{tag} record {t}')
+    env.close()
+
+
+@pytest.mark.gpu
+def test_facade_group_access_render_manual():
+    if not gpu_available():
+        pytest.skip('no GPU')
+    from mfg_amd.factory import Factory
+    env = Factory('large8.yaml', py_seed=3)  # not synced with Python's random: two independent envs
+    env.reset()
+    doors = env['Doors']
+    assert doors.name == 'Doors' and len(doors) == env.spec.c.n_doors
+    assert len(env['Agent']) == env.spec.n_agents
+    assert env.render('rgb_array').shape == (env.spec.H, env.spec.W, 3)
+    assert len(env.render('ansi').splitlines()) == env.spec.H
+    # manual protocol == step on a twin env with the same seed
+    twin = Factory('large8.yaml', py_seed=3)
+    twin.reset()
+    acts = [1] * env.spec.n_agents
+    env.manual_step_init()
+    res = [env.manual_agent_tick(f'Agent[{n}]', a) for n, a in zip(env.spec.agent_names, acts)]
+    env.manual_finalize_init()
+    rew, done, info = env.manual_step_finalize(None)
+    _, obs2, rew2, done2, info2 = twin.step(acts)
+    assert rew == rew2 and done == done2 and info == info2
+    assert (env.manual_get_agent_obs(f'Agent[{env.spec.agent_names[0]}]') == obs2[0]).all()
+    assert res[0].identifier == env.summarize_state()['agents'][0]['action']
+    with pytest.raises(RuntimeError):
+        env.manual_step_init()
+        env.manual_agent_tick(f'Agent[{env.spec.agent_names[1]}]', 0)  # out of list order
+    env.close()
+    twin.close()
