@@ -118,6 +118,28 @@ def cpu_model():
     return 'unknown'
 
 
+def stream_copy_gbs(dev, nbytes=2 << 30, reps=10):
+    """Measured HBM stream-copy bandwidth on this GPU: a device-to-device copy of `nbytes`
+    moves 2 x nbytes; best of `reps` after a warm-up, timed with events on the current stream."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    best = None
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        b.copy_(a)
+        e.record()
+        e.synchronize()
+        t = s.elapsed_time(e) * 1e-3
+        best = t if best is None else min(best, t)
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / best / 1e9
+
+
 def load_pmc(workload):
     """HBM traffic per launch from the committed rocprofv3 PMC summary (profiles/pmc_*.json)."""
     for p in sorted((ROOT / 'profiles').glob('pmc_*.json'), reverse=True):
@@ -260,6 +282,14 @@ def main():
             roof = {"bound": "hbm", "achieved": round(pipe_bytes / mean_call / 1e9, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(pipe_bytes / mean_call / 1e9 / HBM_PEAK_GBS, 5),
                     "traffic": None, "kernel": "mfg_step pipeline", "mean_launch_ms": round(mean_call * 1e3, 3)}
+        try:
+            peak_meas = round(stream_copy_gbs(dev), 1)
+        except RuntimeError:  # not enough free HBM for the 4 GiB copy pair
+            peak_meas = None
+        roof["peak_measured"] = peak_meas
+        roof["peak_measured_how"] = "device-to-device copy of 2 GiB (2 x 2 GiB moved), best of 10"
+        if peak_meas and roof.get("achieved"):
+            roof["frac_of_measured"] = round(roof["achieved"] / peak_meas, 5)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))

@@ -425,31 +425,32 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     const int nacc = popc(m);
     const int inext = icur - nacc, idxn = idx + consumed;
 #ifndef MFG_ABLATE_NOSWAP
-    if (nacc) {
-      const bool acc = lanes(m);
-      const int i = icur - A, j = (int)r;
-      uint16_t* pi = acc ? &perm[i] : sink;
-      int v = (int)*pi;
-      // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
-      // the block's own i range [inext + 1, i)), the last one's V_s. Few forwards (large i): walk them
-      // in ascending s, so V_s is final before it is forwarded to rank icur - j_s (rejected lanes
-      // sharing that rank carry no swap and may take the value harmlessly). Many (small i): a rank
-      // table (tag | lane, keyed by icur - j) gives each draw its forward source and pointer jumping
-      // resolves the chains.
-      u64 cm = ballot(acc && j > inext && j < i);
-      const bool fwd = lanes(cm);
+    // (a chunk with no accepted draw runs the block on the sinks: rare, and one branch less per chunk)
+    const bool acc = lanes(m);
+    const int i = icur - A, j = (int)r;
+    uint16_t* pi = acc ? &perm[i] : sink;
+    int v = (int)*pi;
+    // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
+    // the block's own i range (inext, i)), the last one's V_s. Rare at large i: a single scalar test
+    // skips it. Few forwards: walk them in ascending s, so V_s is final before it is forwarded to rank
+    // icur - j_s (rejected lanes sharing that rank carry no swap and may take the value harmlessly).
+    // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
+    // and pointer jumping resolves the chains.
+    u64 cm = ballot(acc && (unsigned)(j - inext - 1) < (unsigned)(nacc - 1 - A));
+    if (cm) {
       u64 cx = cm;  // clear the RP_SERIAL_FWD lowest forwards: none left <=> few enough (scalar ops only)
 #pragma unroll
       for (int q = 0; q < RP_SERIAL_FWD; q++) cx &= cx - 1;
       if (cx == 0) {
-        while (cm) {
+        do {
           const int s = ffs64(cm);
           cm &= cm - 1;
           const int key = icur - rl(j, s);
           const int vs = rl(v, s);
           v = A == key ? vs : v;
-        }
+        } while (cm);
       } else {
+        const bool fwd = lanes(cm);
         ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
         const uint32_t tag = ctr << 6;
         atomicMax(&ptab[fwd ? icur - j : lane], fwd ? tag | (uint32_t)lane : 0u);  // max with 0: no-op
@@ -462,16 +463,14 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
           if (ptr >= 0) { v = v2; ptr = p2; }
         }
       }
-      // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
-      // The next chunk's MT words are loaded while the exchange is in flight.
-      uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
-      yw = mt[min(idxn, 624) + lane];
-      F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
-      *pi = (uint16_t)F;
-      wave_sync();
-    } else {
-      yw = mt[min(idxn, 624) + lane];
     }
+    // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
+    // The next chunk's MT words are loaded while the exchange is in flight.
+    uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
+    yw = mt[min(idxn, 624) + lane];
+    F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
+    *pi = (uint16_t)F;
+    wave_sync();
 #else
     yw = mt[min(idxn, 624) + lane];
 #endif
