@@ -398,7 +398,8 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
       yw = mt[lane];
     }
     const bool has = lane < 624 - idx;
-    const u64 hasm = ballot(has);
+    const int left = 624 - idx;  // words left in the state (uniform): the lanes that read a real word
+    const u64 hasm = left >= 64 ? ~0ull : (1ull << left) - 1ull;
     const uint32_t y = mt_temper(yw);
     // One bit width per chunk: k = bitlen(icur + 1), and the chunk stops where bitlen(i + 1) would
     // change (i < 2^(k-1) - 1) or at lo. Within it accept <=> A <= c = min(icur - r, span), with
@@ -436,7 +437,7 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     // icur - j_s (rejected lanes sharing that rank carry no swap and may take the value harmlessly).
     // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
     // and pointer jumping resolves the chains.
-    u64 cm = ballot(acc && (unsigned)(j - inext - 1) < (unsigned)(nacc - 1 - A));
+    u64 cm = ballot((unsigned)(j - inext - 1) < (unsigned)(nacc - 1 - A)) & m;
     if (cm) {
       u64 cx = cm;  // clear the RP_SERIAL_FWD lowest forwards: none left <=> few enough (scalar ops only)
 #pragma unroll
