@@ -111,4 +111,10 @@ struct MfgDevSpec {
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)
   int32_t lds_replay_per_wave;  // k_replay slice: [hdr][MT + u16 perm image of the record][sink][tables]
   int32_t replay_mtperm, replay_sink_off, replay_stab_off, replay_stab_n;
+  // Combined obs layers whose members all encode 1.0 (walls, items, pods, drop-offs, destinations,
+  // maintainers, agents) and appear once: the left-to-right f64 sum of 0/1 terms equals the member count,
+  // so k_obs places popc(tags & comb_unit_tags) + popc(agents & comb_agents) instead of a member loop
+  int32_t comb_fast[MFG_MAX_AGENTS];
+  uint32_t comb_unit_tags[MFG_MAX_AGENTS];
+  uint64_t comb_agents[MFG_MAX_AGENTS];
 };

@@ -1887,6 +1887,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   typedef __attribute__((address_space(3))) uint32_t lds_u32;
   lds_u32* dsup = (lds_u32*)((uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE);
   const int ndsup = S->dirt_cap >> 5;
+  // agents on each window cell: [dd][2] u32 (bit b = agent b), filled by a lane-per-agent scatter
+  lds_u32* amw = dsup + ndsup;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
   const int agp = lane < A ? e.agpos()[lane] : -1;
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
@@ -1900,7 +1902,13 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
+    for (int i = lane; i < 2 * dd; i += MFG_WAVE) amw[i] = 0u;
     wave_sync();
+    if (lane < A) {  // scatter the agents into the window's agent masks
+      const int wx = agp / W - ax + r, wy = agp % W - ay + r;
+      if ((unsigned)wx < (unsigned)d && (unsigned)wy < (unsigned)d)
+        atomicOr((uint32_t*)&amw[2 * (wx * d + wy) + (lane >> 5)], 1u << (lane & 31));
+    }
     // ---- ray walk (lane = ray, 64 rays per pass): blocking bits first, then the walk on bitmasks ----
 #ifdef MFG_ABLATE_OB_NORAY
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0u;
@@ -2011,10 +2019,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
         }
         tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
       }
-      u64 amask = 0;
-#ifndef MFG_ABLATE_OB_NOAMASK
-      for (int b = 0; b < A; b++) amask |= (v && rl(agp, b) == cell) ? (1ull << b) : 0ull;
-#endif
+      const int wic = inwin ? wi : 0;
+      const u64 amask = v ? ((u64)amw[2 * wic] | ((u64)amw[2 * wic + 1] << 32)) : 0ull;
       // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
       // 0.4444 open, dirt = amount)
       auto tagv = [&](int tag) -> double {
@@ -2030,6 +2036,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
         double val = 0.0;
         if (kind == MFG_LAYER_TAG) {
           val = tagv(S->s.layers[a][l].tag);
+        } else if (kind == MFG_LAYER_COMBINED && S->comb_fast[a]) {
+          val = (double)(popc(tags & S->comb_unit_tags[a]) + popc(amask & S->comb_agents[a]));
         } else if (kind == MFG_LAYER_COMBINED) {
           const int nc = S->s.combined_n[a];
           for (int q = 0; q < nc; q++) {
@@ -2547,6 +2555,26 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   const int HW = s->H * s->W;
   h.HW = HW; h.nf = s->n_floor; h.nw = s->n_walls; h.nd = s->n_doors; h.A = s->n_agents;
   h.r = s->pomdp_r; h.d = 2 * s->pomdp_r + 1; h.dd = h.d * h.d; h.nrays = s->n_rays;
+  for (int a = 0; a < s->n_agents; a++) {  // combined layers that are plain member counts (MfgDevSpec)
+    uint32_t tm = 0;
+    uint64_t am = 0;
+    bool fast = true;
+    for (int q = 0; q < s->combined_n[a]; q++) {
+      const int t = s->combined_tags[a][q];
+      if (t >= MFG_TAG_AGENT0) {
+        const uint64_t bit = 1ull << (t - MFG_TAG_AGENT0);
+        fast = fast && !(am & bit);
+        am |= bit;
+      } else {
+        const bool unit = t != MFG_TAG_DOORS && t != MFG_TAG_DIRT && t != MFG_TAG_MACHINES;
+        fast = fast && unit && !(tm & (1u << t));
+        tm |= 1u << t;
+      }
+    }
+    h.comb_fast[a] = fast && s->combined_n[a] > 0;
+    h.comb_unit_tags[a] = tm;
+    h.comb_agents[a] = am;
+  }
   if (h.nrays > 4 * MFG_WAVE) { delete e; return fail("more than 256 rays"); }
   h.maxpts = 2 * s->pomdp_r + 2;
   int lmax = 1;
@@ -2615,7 +2643,8 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
   h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
-              4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8;
+              4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
+              8 * h.dd;  // + per-window-cell agent masks (u64)
   // replay kernel slice: [hdr 32 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
