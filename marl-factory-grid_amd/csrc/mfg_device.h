@@ -72,6 +72,16 @@ struct MfgLayout {
 // per-maintainer state ints: [path_n, path_head, next_n, last_serviced, next[mmax + 1]]
 enum { MS_PATH_N = 0, MS_PATH_HEAD, MS_NEXT_N, MS_LAST_SERVICED, MS_NEXT };
 
+// One observation layer of one agent as k_obs places it: value = popc(tags & unit_tags) +
+// popc(agents & agent_bits) (members that encode 1.0, each once), unless a flag asks for more.
+enum { LR_DOOR = 1, LR_DIRT = 2, LR_MACHINE = 4, LR_BATTERY = 8, LR_GLOBALPOS = 16, LR_ORDERED = 32 };
+struct MfgLayerRec {
+  uint32_t unit_tags;  // entity tags (< 16) counted as 1.0
+  uint32_t flags;      // LR_*: door / dirt / machine value of a single-tag layer, regex-bound layers, or a
+                       // Combined layer that needs its ordered left-to-right f64 sum (non-unit members)
+  uint64_t agent_bits; // agents counted as 1.0
+};
+
 struct MfgDevSpec {
   mfg_spec s;  // table pointers inside are HOST pointers: never dereferenced on the device
   int32_t HW, nf, nw, nd, A, r, d, dd, nrays, maxpts, lmax;
@@ -117,4 +127,5 @@ struct MfgDevSpec {
   int32_t comb_fast[MFG_MAX_AGENTS];
   uint32_t comb_unit_tags[MFG_MAX_AGENTS];
   uint64_t comb_agents[MFG_MAX_AGENTS];
+  const MfgLayerRec* lrec;   // [A][lmax] layer records
 };

@@ -2031,25 +2031,30 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
         if (tag == MFG_TAG_MACHINES) return (double)S->s.machine_pause;  // idle forever: encoding 15 (Q18)
         return 1.0;
       };
+      const MfgLayerRec CS* lr = (const MfgLayerRec CS*)S->lrec + (size_t)a * S->lmax;
       for (int l = 0; l < nl; l++) {
-        const int kind = S->s.layers[a][l].kind;
-        double val = 0.0;
-        if (kind == MFG_LAYER_TAG) {
-          val = tagv(S->s.layers[a][l].tag);
-        } else if (kind == MFG_LAYER_COMBINED && S->comb_fast[a]) {
-          val = (double)(popc(tags & S->comb_unit_tags[a]) + popc(amask & S->comb_agents[a]));
-        } else if (kind == MFG_LAYER_COMBINED) {
-          const int nc = S->s.combined_n[a];
-          for (int q = 0; q < nc; q++) {
-            const double tv = tagv(S->s.combined_tags[a][q]);
-            val = q == 0 ? tv : val + tv;
+        const uint32_t ut = lr[l].unit_tags, fl = lr[l].flags;
+        const uint64_t ab = lr[l].agent_bits;
+        double val = (double)(popc(tags & ut) + popc(amask & ab));
+        if (fl) {
+          if (fl & LR_DOOR) {
+            val = tagv(MFG_TAG_DOORS);
+          } else if (fl & LR_DIRT) {
+            val = tagv(MFG_TAG_DIRT);
+          } else if (fl & LR_MACHINE) {
+            val = tagv(MFG_TAG_MACHINES);
+          } else if (fl & LR_ORDERED) {
+            const int nc = S->s.combined_n[a];
+            for (int q = 0; q < nc; q++) {
+              const double tv = tagv(S->s.combined_tags[a][q]);
+              val = q == 0 ? tv : val + tv;
+            }
+          } else if (fl & LR_BATTERY) {
+            val = wi == 0 ? (frozen ? e.fbat()[a] : e.bat()[a]) : 0.0;
+          } else {  // LR_GLOBALPOS
+            const int gp = frozen ? e.fgp()[a] : apos;
+            val = wi == 0 ? (double)(gp / W) / (double)H : (wi == 1 ? (double)(gp % W) / (double)W : 0.0);
           }
-        } else if (kind == MFG_LAYER_BATTERY) {
-          if (wi == 0) val = frozen ? e.fbat()[a] : e.bat()[a];
-        } else if (kind == MFG_LAYER_GLOBALPOS) {
-          const int gp = frozen ? e.fgp()[a] : apos;
-          if (wi == 0) val = (double)(gp / W) / (double)H;
-          if (wi == 1) val = (double)(gp % W) / (double)W;
         }
         if (inwin) out_a[(size_t)l * dd + wi] = (OT)val;
       }
@@ -2713,6 +2718,30 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   rc |= upload(e, base_map.data(), base_map.size(), &h.base_map);
   rc |= upload(e, base_map8.data(), base_map8.size(), &h.base_map8);
   rc |= upload(e, cell_f.data(), cell_f.size(), &h.cell_f);
+  {  // layer records (MfgLayerRec)
+    std::vector<MfgLayerRec> lrec((size_t)h.A * h.lmax);
+    for (int a = 0; a < h.A; a++)
+      for (int l = 0; l < s->n_layers[a]; l++) {
+        MfgLayerRec& R = lrec[(size_t)a * h.lmax + l];
+        R = MfgLayerRec{0u, 0u, 0ull};
+        const int kind = s->layers[a][l].kind, tag = s->layers[a][l].tag;
+        if (kind == MFG_LAYER_TAG) {
+          if (tag >= MFG_TAG_AGENT0) R.agent_bits = 1ull << (tag - MFG_TAG_AGENT0);
+          else if (tag == MFG_TAG_DOORS) R.flags = LR_DOOR;
+          else if (tag == MFG_TAG_DIRT) R.flags = LR_DIRT;
+          else if (tag == MFG_TAG_MACHINES) R.flags = LR_MACHINE;
+          else R.unit_tags = 1u << tag;
+        } else if (kind == MFG_LAYER_COMBINED) {
+          if (h.comb_fast[a]) { R.unit_tags = h.comb_unit_tags[a]; R.agent_bits = h.comb_agents[a]; }
+          else R.flags = LR_ORDERED;
+        } else if (kind == MFG_LAYER_BATTERY) {
+          R.flags = LR_BATTERY;
+        } else if (kind == MFG_LAYER_GLOBALPOS) {
+          R.flags = LR_GLOBALPOS;
+        }
+      }
+    rc |= upload(e, lrec.data(), lrec.size(), &h.lrec);
+  }
   rc |= upload(e, node_ok.data(), node_ok.size(), &h.node_ok);
   rc |= upload(e, wd.data(), wd.size(), &h.wd_pairs);
   if (rc) { delete e; return -1; }
