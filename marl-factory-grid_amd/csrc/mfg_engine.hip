@@ -703,6 +703,33 @@ __device__ int global_count(const Env& e, int cell) {
   return n;
 }
 
+// global_count for one cell per lane (each lane its own `cell`, -1 = none): the same terms as
+// global_count, counted by uniform loops over the group tables (broadcast LDS reads) instead of one
+// ballot round per cell
+__device__ int global_count_lanes(const Env& e, int cell) {
+  SpecP S = e.S;
+  const bool ok = cell >= 0;
+  const int c = ok ? cell : 0;
+  int n = ok && S->level[c] == 1;
+  const int d = ok ? door_idx(e, c) : -1;
+  if (d >= 0 && (e.door()[d] & DW_PRESENT)) n++;
+  for (int b = 0; b < S->A; b++) n += e.agpos()[b] == cell;
+  auto grp = [&](const int* tbl, int cnt) {
+    for (int i = 0; i < cnt; i++) {
+      const int w = tbl[i];
+      n += (EW_POS(w) == cell && (w & EW_PRESENT)) ? 1 : 0;
+    }
+  };
+  grp(e.items(), e.H(H_N_ITEMS));
+  grp(e.pods(), e.H(H_N_PODS));
+  grp(e.drops(), e.H(H_N_DROPS));
+  grp(e.dests(), e.H(H_N_DESTS));
+  grp(e.dirtpos(), e.H(H_N_DIRT));
+  if (S->mmax) grp(e.machines(), e.H(H_N_MACHINES));
+  if (S->kmax) grp(e.maints(), e.H(H_N_MAINTS));
+  return ok ? n : 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // spawn-position queries (global_entities.py:77-121)
 // ------------------------------------------------------------------------------------------------
@@ -1333,11 +1360,7 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
   if (op == MFG_RULE_DOOR_AUTOCLOSE) {  // doors/rules.py:20-28, doors/entitites.py:107-122
     if (S->nd > 0) {
       const int nd = S->nd;
-      int cnt = 0;
-      for (int d = 0; d < nd; d++) {  // global_count uses ballots: evaluate per door uniformly
-        int c = global_count(e, S->door_cells[d]);
-        if (e.lane == d) cnt = c;
-      }
+      const int cnt = global_count_lanes(e, e.lane < nd ? S->door_cells[e.lane < nd ? e.lane : 0] : -1);  // lane = door
       wave_sync();
       if (e.lane < nd) {
         int w = e.door()[e.lane];
