@@ -730,6 +730,21 @@ __device__ int global_count_lanes(const Env& e, int cell) {
   return ok ? n : 0;
 }
 
+// colliders_at for one cell per lane (-1 = none), by uniform loops over agents and maintainers
+__device__ int colliders_lanes(const Env& e, int cell) {
+  SpecP S = e.S;
+  const bool ok = cell >= 0;
+  const int c = ok ? cell : 0;
+  int n = (ok && S->level[c] == 1) + (ok && present_closed_door(e, c) ? 1 : 0);
+  for (int b = 0; b < S->A; b++) n += e.agpos()[b] == cell;
+  const int nk = S->kmax ? e.H(H_N_MAINTS) : 0;
+  for (int i = 0; i < nk; i++) {
+    const int w = e.maints()[i];
+    n += (EW_POS(w) == cell && (w & EW_PRESENT)) ? 1 : 0;
+  }
+  return ok ? n : 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // spawn-position queries (global_entities.py:77-121)
 // ------------------------------------------------------------------------------------------------
@@ -1478,17 +1493,23 @@ __device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
         if (id < 64) used |= 1ull << id;
       }
     };
-    for (int d = 0; d < S->nd; d++) {
+    // candidate cells first, lane-parallel (lane = door, then lane = agent); the ordered passes below
+    // visit only cells with >= 2 colliders (usually none)
+    const int nd = S->nd;
+    const u64 dcand = ballot(e.lane < nd && colliders_lanes(e, e.lane < nd ? S->door_cells[e.lane < nd ? e.lane : 0] : -1) >= 2);
+    const int myp = e.lane < A ? e.agpos()[e.lane] : -1;
+    const u64 acand = ballot(e.lane < A && door_idx(e, myp < 0 ? 0 : myp) < 0 && colliders_lanes(e, myp) >= 2);
+    for (u64 dm = dcand; dm; dm &= dm - 1) {
+      const int d = ffs64(dm);
       const int cell = S->door_cells[d];
-      if (colliders_at(e, cell) < 2) continue;
       hit = true;
       if (present_closed_door(e, cell) && !((used >> d) & 1)) { o.door_coll |= 1ull << d; used |= 1ull << d; }
       if (e.lane < A && e.agpos()[e.lane] == cell) agres = true;
       maint_results(cell);
     }
-    for (int a = 0; a < A; a++) {
+    for (u64 am = acand; am; am &= am - 1) {
+      const int a = ffs64(am);
       const int cell = uni(e.agpos()[a]);
-      if (door_idx(e, cell) >= 0 || colliders_at(e, cell) < 2) continue;
       hit = true;
       if (e.lane == a) agres = true;
       maint_results(cell);
