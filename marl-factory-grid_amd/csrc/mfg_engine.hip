@@ -411,7 +411,8 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     const uint32_t r = y >> sh;
     const int c = has ? min(icur - (int)r, span) : -1;
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
-    u64 m = ballot(c >= 63);
+    // (A_l <= l, so c_l >= l accepts for sure)
+    u64 m = ballot(c >= lane);
 #ifdef MFG_ABLATE_NOJACOBI
     m = ballot(mbcnt(ballot(c >= 0)) <= c);
     if (0)
