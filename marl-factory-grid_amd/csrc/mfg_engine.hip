@@ -386,20 +386,31 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
   int idx = e.H(H_MT_IDX);
   int icur = e.S->nf - 1;
   uint32_t ctr = (uint32_t)uni((int)e.stab[RP_CTR]);
-  // raw MT words of the next chunk, loaded one chunk ahead (lanes past the state read the words after
-  // it, inside the slice, and are discarded)
-  uint32_t yw = mt[min(idx, 624) + lane];
+  // Every chunk reads 64 words. Near the end of the state (idx > 560) the lanes past word 623 compute
+  // the next state's first words directly from the current one (new[i] = mix(mt[i], mt[i+1],
+  // mt[i+397]) for i < 227, the twist's first phase), so a chunk may run past the end: idx then exceeds
+  // 624 and the in-place twist that follows (idx -= 624) writes the same words. Away from the end the
+  // raw words of the next chunk are loaded one chunk ahead.
+  uint32_t yw = 0;
+  bool pre = false;
   while (icur >= lo) {
     if (idx >= 624) {
 #ifndef MFG_ABLATE_NOTWIST
       mt_twist(e);
 #endif
-      idx = 0;
-      yw = mt[lane];
+      idx -= 624;
+      pre = false;
     }
-    const bool has = lane < 624 - idx;
-    const int left = 624 - idx;  // words left in the state (uniform): the lanes that read a real word
-    const u64 hasm = left >= 64 ? ~0ull : (1ull << left) - 1ull;
+    if (!pre) {
+      const int jw = idx + lane;
+      if (idx <= 560) {
+        yw = mt[jw];
+      } else {
+        const int jn = jw >= 624 ? jw - 624 : 0;
+        const uint32_t nw = mt_mix(mt[jn], mt[jn + 1], mt[jn + 397]);
+        yw = jw < 624 ? mt[jw < 624 ? jw : 0] : nw;
+      }
+    }
     const uint32_t y = mt_temper(yw);
     // One bit width per chunk: k = bitlen(icur + 1), and the chunk stops where bitlen(i + 1) would
     // change (i < 2^(k-1) - 1) or at lo. Within it accept <=> A <= c = min(icur - r, span), with
@@ -409,7 +420,7 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     const int sh = __clz(icur + 1);
     const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank this chunk may take
     const uint32_t r = y >> sh;
-    const int c = has ? min(icur - (int)r, span) : -1;
+    const int c = min(icur - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
     // (A_l <= l, so c_l >= l accepts for sure)
     u64 m = ballot(c >= lane);
@@ -423,7 +434,7 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
       m = m2;
     }
     const int A = mbcnt(m);
-    const int consumed = popc(ballot(A <= span) & hasm);
+    const int consumed = popc(ballot(A <= span));
     const int nacc = popc(m);
     const int inext = icur - nacc, idxn = idx + consumed;
 #ifndef MFG_ABLATE_NOSWAP
@@ -469,15 +480,21 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
     // The next chunk's MT words are loaded while the exchange is in flight.
     uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
-    yw = mt[min(idxn, 624) + lane];
+    pre = idxn <= 560;
+    if (pre) yw = mt[idxn + lane];
     F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
     *pi = (uint16_t)F;
     wave_sync();
 #else
-    yw = mt[min(idxn, 624) + lane];
+    pre = idxn <= 560;
+    if (pre) yw = mt[idxn + lane];
 #endif
     icur = inext;
     idx = idxn;
+  }
+  if (idx > 624) {  // words of the next state were consumed: make the state canonical (CPython's mti)
+    mt_twist(e);
+    idx -= 624;
   }
   if (lane == 0) e.stab[RP_CTR] = ctr;
   e.setH(H_MT_IDX, idx);
