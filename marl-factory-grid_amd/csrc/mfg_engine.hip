@@ -126,6 +126,11 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 18);
   return y;
 }
+__device__ __forceinline__ uint32_t mt_temper3(uint32_t y) {  // mt_temper without its last step
+  y ^= (y >> 11);
+  y = XOR_AND(y, y << 7, 0x9d2c5680u);
+  return XOR_AND(y, y << 15, 0xefc60000u);
+}
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
   const uint32_t y = __builtin_amdgcn_bitop3_b32(a, b, MT_UPPER, 0xE4);  // (a & UPPER) | (b & LOWER)
   const uint32_t odd = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);       // y & 1 == b & 1, as a mask
@@ -352,10 +357,10 @@ __device__ __forceinline__ uint32_t lds_xchg_u16(uint16_t* p, uint32_t v) {
 // The same exchange split in two: issue (returns the raw old dword, not yet waited for), then wait
 // (tied to that value, so nothing reads it early) and extract the 16-bit half. LDS operations complete
 // in issue order, so the compiler's own counted lgkmcnt waits stay conservative around it.
-__device__ __forceinline__ uint32_t lds_xchg_u16_issue(uint16_t* p, uint32_t v) {
+__device__ __forceinline__ uint32_t lds_xchg_u16_issue(uint16_t* p, uint32_t v) {  // v < 65536
   const uint32_t a = (uint32_t)(uintptr_t)p;
   const uint32_t sh = (a & 2u) << 3;
-  const uint32_t mask = 0xFFFFu << sh, data = (v & 0xFFFFu) << sh;
+  const uint32_t mask = 0xFFFFu << sh, data = v << sh;
   uint32_t old;
   asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(old) : "v"(a & ~3u), "v"(mask), "v"(data) : "memory");
   return old;
@@ -375,9 +380,12 @@ __device__ __forceinline__ uint32_t lds_xchg_u16_wait(uint32_t old, uint16_t* p)
 #define RP_HDR_N 8  // header ints k_replay keeps in its slice (H_DEBT, H_MT_IDX)
 static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice");
 #ifndef RP_SERIAL_FWD
-#define RP_SERIAL_FWD 2  // blocks with at most this many forwards resolve them serially (no LDS table)
+#define RP_SERIAL_FWD 4  // blocks with at most this many forwards resolve them serially (no LDS table)
 #endif
-__device__ void replay_shuffle(const Env& e, uint16_t* perm) {
+// TOP14: every width k = bitlen(i + 1) is <= 14 (nf < 16384), so r = y >> (32 - k) reads only bits
+// 18..31 of the tempered word, which the last tempering step (y ^= y >> 18) leaves unchanged.
+template <bool TOP14>
+__device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
   uint16_t* sink = (uint16_t*)e.scratch + lane;  // 128 B: one u16 per lane
@@ -389,19 +397,18 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
   // Every chunk reads 64 words. Near the end of the state (idx > 560) the lanes past word 623 compute
   // the next state's first words directly from the current one (new[i] = mix(mt[i], mt[i+1],
   // mt[i+397]) for i < 227, the twist's first phase), so a chunk may run past the end: idx then exceeds
-  // 624 and the in-place twist that follows (idx -= 624) writes the same words. Away from the end the
-  // raw words of the next chunk are loaded one chunk ahead.
-  uint32_t yw = 0;
-  bool pre = false;
+  // 624 and the in-place twist that follows (idx -= 624) writes the same words. Away from the end
+  // (idx <= 560) the raw words of the next chunk are loaded one chunk ahead, so whether this chunk's
+  // words are already in yw follows from idx alone (a twisted state had idx >= 624 > 560).
+  uint32_t yw = idx <= 560 ? mt[idx + lane] : 0u;
   while (icur >= lo) {
-    if (idx >= 624) {
+    if (idx > 560) {
+      if (idx >= 624) {
 #ifndef MFG_ABLATE_NOTWIST
-      mt_twist(e);
+        mt_twist(e);
 #endif
-      idx -= 624;
-      pre = false;
-    }
-    if (!pre) {
+        idx -= 624;
+      }
       const int jw = idx + lane;
       if (idx <= 560) {
         yw = mt[jw];
@@ -411,15 +418,15 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
         yw = jw < 624 ? mt[jw < 624 ? jw : 0] : nw;
       }
     }
-    const uint32_t y = mt_temper(yw);
+    const uint32_t y = TOP14 ? mt_temper3(yw) : mt_temper(yw);
     // One bit width per chunk: k = bitlen(icur + 1), and the chunk stops where bitlen(i + 1) would
     // change (i < 2^(k-1) - 1) or at lo. Within it accept <=> A <= c = min(icur - r, span), with
     // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
     // start the next chunk). So every chunk takes the same branch-free path, power-of-two crossings
     // and the i < 64 tail included.
     const int sh = __clz(icur + 1);
-    const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank this chunk may take
-    const uint32_t r = y >> sh;
+    const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
+    uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
     // (A_l <= l, so c_l >= l accepts for sure)
@@ -428,12 +435,13 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     m = ballot(mbcnt(ballot(c >= 0)) <= c);
     if (0)
 #endif
+    int A;
     for (;;) {
-      const u64 m2 = ballot(mbcnt(m) <= c);
+      A = mbcnt(m);
+      const u64 m2 = ballot(A <= c);
       if (m2 == m) break;
       m = m2;
     }
-    const int A = mbcnt(m);
     const int consumed = popc(ballot(A <= span));
     const int nacc = popc(m);
     const int inext = icur - nacc, idxn = idx + consumed;
@@ -441,7 +449,8 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     // (a chunk with no accepted draw runs the block on the sinks: rare, and one branch less per chunk)
     const bool acc = lanes(m);
     const int i = icur - A, j = (int)r;
-    uint16_t* pi = acc ? &perm[i] : sink;
+    uint16_t* const ptop = perm + icur;  // wave-uniform
+    uint16_t* pi = acc ? ptop - A : sink;
     int v = (int)*pi;
     // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
     // the block's own i range (inext, i)), the last one's V_s. Rare at large i: a single scalar test
@@ -449,15 +458,12 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     // icur - j_s (rejected lanes sharing that rank carry no swap and may take the value harmlessly).
     // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
     // and pointer jumping resolves the chains.
-    u64 cm = ballot((unsigned)(j - inext - 1) < (unsigned)(nacc - 1 - A)) & m;
+    u64 cm = ballot(j > inext) & ballot(j < i) & m;
     if (cm) {
-      u64 cx = cm;  // clear the RP_SERIAL_FWD lowest forwards: none left <=> few enough (scalar ops only)
-#pragma unroll
-      for (int q = 0; q < RP_SERIAL_FWD; q++) cx &= cx - 1;
-      if (cx == 0) {
+      if (popc(cm) <= RP_SERIAL_FWD) {
         do {
           const int s = ffs64(cm);
-          cm &= cm - 1;
+          cm &= ~(1ull << s);
           const int key = icur - rl(j, s);
           const int vs = rl(v, s);
           v = A == key ? vs : v;
@@ -480,14 +486,12 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
     // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
     // The next chunk's MT words are loaded while the exchange is in flight.
     uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
-    pre = idxn <= 560;
-    if (pre) yw = mt[idxn + lane];
+    if (idxn <= 560) yw = mt[idxn + lane];
     F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
     *pi = (uint16_t)F;
     wave_sync();
 #else
-    pre = idxn <= 560;
-    if (pre) yw = mt[idxn + lane];
+    if (idxn <= 560) yw = mt[idxn + lane];
 #endif
     icur = inext;
     idx = idxn;
@@ -499,6 +503,10 @@ __device__ void replay_shuffle(const Env& e, uint16_t* perm) {
   if (lane == 0) e.stab[RP_CTR] = ctr;
   e.setH(H_MT_IDX, idx);
   wave_sync();
+}
+__device__ __forceinline__ void replay_shuffle(const Env& e, uint16_t* perm) {
+  if (e.S->replay_top14) replay_shuffle_t<true>(e, perm);
+  else replay_shuffle_t<false>(e, perm);
 }
 
 // random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
@@ -2372,7 +2380,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, cons
 __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, uint8_t* state, long long B) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
-  const int wid = threadIdx.x >> 6;
+  const int wid = uni(threadIdx.x >> 6);  // wave-uniform: the slice addresses become scalar
   const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
   uint8_t* rec = state + (size_t)env * S->L.size;
@@ -2720,6 +2728,8 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
     h.replay_stab_off = h.replay_sink_off + 2 * MFG_WAVE;  // u16 sinks (replay_shuffle, mt_twist)
     h.replay_stab_n = h.xchg_ordered ? RP_STAB_N : MFG_STAB_N;
     h.lds_replay_per_wave = align_up(h.replay_stab_off + 4 * h.replay_stab_n, 16);
+    const char* ft = getenv("MFG_REPLAY_FULL_TEMPER");  // tests: force the full-temper path
+    h.replay_top14 = h.nf < 16384 && !(ft && ft[0] == '1');
   }
   pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
   // static tables
