@@ -1975,18 +1975,20 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
   const int nT = e.H(H_N_DIRT);
   const int npass = (S->nrays + MFG_WAVE - 1) / MFG_WAVE;
+  const int pA0 = lane < npairs ? pairs.get(lane, 0) : 0, pB0 = lane < npairs ? pairs.get(lane, 1) : 0;
+  // agent and ray-origin coordinates: one vector division per render, read per agent with v_readlane
+  const int agx = agp / W, agy = agp % W, orgx = org_l / W, orgy = org_l % W;
   for (int a = 0; a < A; a++) {
     const int apos = rl(agp, a);
-    const int ax = apos / W, ay = apos % W;
-    const int org = rl(org_l, a);
-    const int ox = org / W, oy = org % W;
+    const int ax = rl(agx, a), ay = rl(agy, a);
+    const int ox = rl(orgx, a), oy = rl(orgy, a);
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
     for (int i = lane; i < 2 * dd; i += MFG_WAVE) amw[i] = 0u;
     wave_sync();
     if (lane < A) {  // scatter the agents into the window's agent masks
-      const int wx = agp / W - ax + r, wy = agp % W - ay + r;
+      const int wx = agx - ax + r, wy = agy - ay + r;
       if ((unsigned)wx < (unsigned)d && (unsigned)wy < (unsigned)d)
         atomicOr((uint32_t*)&amw[2 * (wx * d + wy) + (lane >> 5)], 1u << (lane & 31));
     }
@@ -2021,11 +2023,14 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
       // first-visit entries are never read (placement tests the grid bounds, pairs are in-grid cells)
       const uint32_t vism = walked & ~cutm;
       uint32_t* sink = (uint32_t*)(wsup + ((dd + 15) & ~15)) + lane;
+      // point 0 of every ray is the origin (checked at mfg_create) and always visible: its entry is
+      // ray 0's rank 0, stored once below instead of a 64-lane same-address atomic
 #pragma unroll
-      for (int p = 0; p < MAXPTS; p++)
+      for (int p = 1; p < MAXPTS; p++)
         atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + d) * fw + ray.dy(p) + d] : sink,
                   (uint32_t)(ray_id * 32 + p));
     }
+    if (lane == 0) fv[d * fw + d] = 0u;
     wave_sync();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     Sup sup;
@@ -2035,12 +2040,15 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
     sup.dsup = dsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
-      const int pA = q < npairs ? pairs.get(q, 0) : 0, pB = q < npairs ? pairs.get(q, 1) : 0;
+      // the first pass's pair cells stay in registers across agents (the usual single pass)
+      const int pA = q0 == 0 ? pA0 : (q < npairs ? pairs.get(q, 0) : 0);
+      const int pB = q0 == 0 ? pB0 : (q < npairs ? pairs.get(q, 1) : 0);
       const int xA = (pA >> 16) - ox + d, yA = (pA & 0xFFFF) - oy + d;
       const int xB = (pB >> 16) - ox + d, yB = (pB & 0xFFFF) - oy + d;
-      const bool nearq = q < npairs && (unsigned)xA < (unsigned)fw && (unsigned)yA < (unsigned)fw &&
-                         (unsigned)xB < (unsigned)fw && (unsigned)yB < (unsigned)fw;
-      const uint32_t rA = nearq ? fv[xA * fw + yA] : 0xFFFFFFFFu, rB = nearq ? fv[xB * fw + yB] : 0xFFFFFFFFu;
+      const bool nearq = (q < npairs) & ((unsigned)xA < (unsigned)fw) & ((unsigned)yA < (unsigned)fw) &
+                         ((unsigned)xB < (unsigned)fw) & ((unsigned)yB < (unsigned)fw);
+      const uint32_t rA0 = fv[nearq ? xA * fw + yA : 0], rB0 = fv[nearq ? xB * fw + yB : 0];
+      const uint32_t rA = nearq ? rA0 : 0xFFFFFFFFu, rB = nearq ? rB0 : 0xFFFFFFFFu;
       u64 hm = ballot(rA != 0xFFFFFFFFu && rB != 0xFFFFFFFFu);
       while (hm) {
         const int L = ffs64(hm);
@@ -2148,7 +2156,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
             val = wi == 0 ? (double)(gp / W) / (double)H : (wi == 1 ? (double)(gp % W) / (double)W : 0.0);
           }
         }
-        if (inwin) out_a[(size_t)l * dd + wi] = (OT)val;
+        // non-temporal: the obs stream is not re-read by this GPU (k_obs 0.518 -> 0.513 ms, k_logic
+        // 0.298 -> 0.291 ms at C3: less L2 pollution)
+        if (inwin) __builtin_nontemporal_store((OT)val, &out_a[(size_t)l * dd + wi]);
       }
     }
   }
@@ -2796,6 +2806,9 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
   for (int r = 0; r < h.nrays; r++) {
     const int p0 = s->ray_off[r], p1 = s->ray_off[r + 1];
     if (p1 - p0 > h.maxpts) { delete e; return fail("ray longer than 2r+2 points"); }
+    if (p1 - p0 < 1 || s->ray_pts[2 * p0] != 0 || s->ray_pts[2 * p0 + 1] != 0) {  // k_obs relies on it
+      delete e; return fail("every ray must start at the origin (bresenham_loop, ray_caster.py:141-199)");
+    }
     rlen[r] = (uint8_t)(p1 - p0);
     for (int p = p0 + 1; p < p1; p++)
       if (s->ray_pts[2 * p] != s->ray_pts[2 * p - 2] && s->ray_pts[2 * p + 1] != s->ray_pts[2 * p - 1])
