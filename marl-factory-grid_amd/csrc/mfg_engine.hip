@@ -2120,7 +2120,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
         tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
       }
       const int wic = inwin ? wi : 0;
-      const u64 amask = v ? ((u64)amw[2 * wic] | ((u64)amw[2 * wic + 1] << 32)) : 0ull;
+      const u64 amraw = (u64)amw[2 * wic] | ((u64)amw[2 * wic + 1] << 32);
+      const u64 amask = v ? amraw : 0ull;
       // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
       // 0.4444 open, dirt = amount)
       auto tagv = [&](int tag) -> double {
@@ -2135,8 +2136,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
       for (int l = 0; l < nl; l++) {
         const uint32_t ut = lr[l].unit_tags, fl = lr[l].flags;
         const uint64_t ab = lr[l].agent_bits;
-        double val = (double)(popc(tags & ut) + popc(amask & ab));
+        OT out = (OT)(popc(tags & ut) + popc(amask & ab));  // a small count: exact in OT
         if (fl) {
+          double val = 0.0;
           if (fl & LR_DOOR) {
             val = tagv(MFG_TAG_DOORS);
           } else if (fl & LR_DIRT) {
@@ -2155,10 +2157,11 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
             const int gp = frozen ? e.fgp()[a] : apos;
             val = wi == 0 ? (double)(gp / W) / (double)H : (wi == 1 ? (double)(gp % W) / (double)W : 0.0);
           }
+          out = (OT)val;
         }
         // non-temporal: the obs stream is not re-read by this GPU (k_obs 0.518 -> 0.513 ms, k_logic
         // 0.298 -> 0.291 ms at C3: less L2 pollution)
-        if (inwin) __builtin_nontemporal_store((OT)val, &out_a[(size_t)l * dd + wi]);
+        if (inwin) __builtin_nontemporal_store(out, &out_a[(size_t)l * dd + wi]);
       }
     }
   }
