@@ -10,6 +10,9 @@
 //
 // See mfg_device.h for the execution model (one wavefront per env).
 #include <hip/hip_runtime.h>
+#ifndef MFG_OBS_NT
+#define MFG_OBS_NT 1  // k_obs writes the observations with non-temporal stores
+#endif
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -2159,9 +2162,16 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
           }
           out = (OT)val;
         }
-        // non-temporal: the obs stream is not re-read by this GPU (k_obs 0.518 -> 0.513 ms, k_logic
-        // 0.298 -> 0.291 ms at C3: less L2 pollution)
+        // non-temporal: the obs stream is not re-read by this GPU (k_obs 0.500 -> 0.493 ms, k_logic
+        // 0.298 -> 0.291 ms at C3: less L2 pollution). WRITE_SIZE counts 1.34x the algorithmic obs bytes
+        // for these stores (1.00x with MFG_OBS_NT=0): the 49-lane layer rows are not 64-B aligned.
+        // Packing rows into aligned 64-lane stores (ds_bpermute) cut that to 1.14x but cost 67 VGPRs
+        // and k_obs 0.494 -> 0.543 ms, so it was dropped (k_obs).
+#if MFG_OBS_NT
         if (inwin) __builtin_nontemporal_store(out, &out_a[(size_t)l * dd + wi]);
+#else
+        if (inwin) out_a[(size_t)l * dd + wi] = out;
+#endif
       }
     }
   }
