@@ -33,8 +33,10 @@ for _p in (ROOT / 'marl-factory-grid_amd', ROOT / 'oracle', ROOT / 'tests'):
     if str(_p) not in sys.path:
         sys.path.insert(0, str(_p))
 
-ALGO_BYTES_PER_ENV_STEP = 11391  # 415 B state/IO + 10,976 B dense fp32 obs (C3)
+ALGO_BYTES_PER_ENV_STEP = 11391  # 415 B state/IO + 10,976 B dense fp32 obs (C3); f64 obs: 22,367
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CU_CLOCK_HZ, N_CU = 2.4e9, 256   # MI355X: 256 CUs, 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+BOX_CPU_SHARE = 16               # host cores the GPU box allots one GPU (worker pools are sized to it)
 METRIC = "env-steps/sec (whole node), 8-agent 'large' level, batch 65536, 1/2/4/8 MI355X"
 
 
@@ -161,7 +163,12 @@ def main():
     ap.add_argument('--batch', type=int, default=65536, help='envs per GPU')
     ap.add_argument('--config', default='large8.yaml')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
-    ap.add_argument('--cpu-workers', type=int, default=0, help='0 = min(16, host cores)')
+    ap.add_argument('--cpu-workers', type=int, default=0,
+                    help='0 = min(16, affinity cores): the GPU box allots 16 host cores per GPU')
+    ap.add_argument('--obs-dtype', choices=['f32', 'f64'], default='f32',
+                    help='obs precision of the headline line (the reference returns f64 obs, Q25)')
+    ap.add_argument('--alt-steps', type=int, default=None,
+                    help='steps of the second measurement with the other obs dtype (default: --steps; 0 = off)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-profile', action='store_true', help='no per-kernel HIP events in the timed region')
     args = ap.parse_args()
@@ -184,7 +191,8 @@ def main():
     dev = torch.device('cuda', local)
     eng = Engine(spec, B, device=local)
     env_base, _ = env_range(rank, world, B)
-    obs = torch.zeros((F,) + eng.obs_shape(), dtype=torch.float32, device=dev)
+    obs_t = torch.float64 if args.obs_dtype == 'f64' else torch.float32
+    obs = torch.zeros((F,) + eng.obs_shape(), dtype=obs_t, device=dev)
     rew = torch.zeros((F, B, A), dtype=torch.float64, device=dev)
     done = torch.zeros((F, B), dtype=torch.uint8, device=dev)
     ev_a = torch.zeros((F, B, A), dtype=torch.uint8, device=dev)
@@ -195,16 +203,21 @@ def main():
     step_no = 0
     episodes = torch.zeros((), dtype=torch.float64, device=dev)
 
-    def run(n, events=None):
+    def run(n, events=None, profile=False, obs_buf=None):
+        """n steps in calls of F (the last call may be shorter). Per-kernel HIP events are recorded only
+        around full-K calls, so the per-launch roofline figures are always those of K=F launches."""
         nonlocal step_no
         done_steps = 0
         while done_steps < n:
             k = min(F, n - done_steps)
+            if profile:
+                eng.profile(k == F)
             if events is not None:
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record(stream)
             eng.step(k, actions=None, philox_seed=12345, env_base=env_base, step_base=step_no, reward=rew, done=done,
-                     obs=obs, ev_act=ev_a, ev_watch=ev_w, ev_misc=ev_m, auto_reset=True)
+                     obs=obs if obs_buf is None else obs_buf, ev_act=ev_a, ev_watch=ev_w, ev_misc=ev_m,
+                     auto_reset=True)
             if events is not None:
                 e.record(stream)
                 events.append((s, e, k))
@@ -217,10 +230,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     calls = []
-    eng.profile(not args.no_profile)
     eng.profile_read()
     t0 = time.perf_counter()
-    run(args.steps, calls)
+    run(args.steps, calls, profile=not args.no_profile)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -236,13 +248,44 @@ def main():
         dist.all_reduce(episodes)  # optional metrics all-reduce (tiny, latency-bound)
     total = B * world * args.steps
     value = total / elapsed
+    # the same workload with the other obs precision (the reference's own obs are f64, Q25), timed the same way
+    alt = None
+    alt_steps = args.steps if args.alt_steps is None else args.alt_steps
+    if alt_steps > 0:
+        alt_dtype = 'f32' if args.obs_dtype == 'f64' else 'f64'
+        obs_alt = torch.zeros((F,) + eng.obs_shape(), dtype=torch.float64 if alt_dtype == 'f64' else torch.float32,
+                              device=dev)
+        run(F, obs_buf=obs_alt)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        run(alt_steps, obs_buf=obs_alt)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el2 = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([el2], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        alt_obs_bytes = sum(spec.n_layers) * spec.d * spec.d * (8 if alt_dtype == 'f64' else 4)
+        alt_step_bytes = core_bytes(spec) + alt_obs_bytes
+        alt_value = B * world * alt_steps / el2
+        alt = {"obs": alt_dtype, "value": round(alt_value, 1), "unit": "env-steps/s", "steps": alt_steps,
+               "ms_per_step": round(el2 / alt_steps * 1e3, 4), "algo_bytes_per_env_step": alt_step_bytes,
+               "pipeline_GBs": round(alt_value / world * alt_step_bytes / 1e9, 2),
+               "pipeline_frac": round(alt_value / world * alt_step_bytes / 1e9 / HBM_PEAK_GBS, 5)}
+        del obs_alt
     if rank == 0:
         full = [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls if k == F] or \
                [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls]
         mean_call = sum(t for t, _ in full) / len(full)
         k_call = full[0][1]
-        obs_bytes = A * spec.n_layers[0] * spec.d * spec.d * 4 if len(set(spec.n_layers)) == 1 else \
-            sum(spec.n_layers[a] for a in range(A)) * spec.d * spec.d * 4
+        obs_el = 8 if args.obs_dtype == 'f64' else 4
+        obs_bytes = sum(spec.n_layers[a] for a in range(A)) * spec.d * spec.d * obs_el
         busy = sum(ms for ms, n in prof.values())
         kernels = {}
         for name, (ms, n) in prof.items():
@@ -259,11 +302,25 @@ def main():
                              "algo_bytes_per_launch": per_launch,
                              "achieved_GBs": round(per_launch / (mean_ms * 1e-3) / 1e9, 2) if per_launch else None}
         dom = max(kernels, key=lambda k: prof[k][0]) if kernels else None
-        workload = f"{Path(args.config).stem}_b{B}_f{F}"
+        workload = f"{Path(args.config).stem}_b{B}_f{F}" + ('_f64' if args.obs_dtype == 'f64' else '')
         pmc = load_pmc(workload)
         traffic = None
         if pmc and dom and dom in pmc.get('hbm_bytes_per_launch', {}):
             traffic = pmc['hbm_bytes_per_launch'][dom]
+        if pmc:  # issue rates per kernel from the committed PMC pass, against this run's launch time
+            for name, kd in kernels.items():
+                c = pmc.get('kernels', {}).get(name)
+                if not c:
+                    continue
+                cu_cycles = kd["mean_launch_ms"] * 1e-3 * CU_CLOCK_HZ * N_CU
+                kd["pmc"] = {"source": pmc.get('tag'),
+                             "hbm_bytes_per_launch": round(c.get('hbm_bytes', 0)),
+                             "traffic_over_algo": round(c['hbm_bytes'] / kd["algo_bytes_per_launch"], 3)
+                             if kd.get("algo_bytes_per_launch") and c.get('hbm_bytes') else None,
+                             "valu_per_cu_cycle": round(c['SQ_INSTS_VALU'] / cu_cycles, 3),
+                             "salu_per_cu_cycle": round(c['SQ_INSTS_SALU'] / cu_cycles, 3),
+                             "lds_per_cu_cycle": round(c['SQ_INSTS_LDS'] / cu_cycles, 3),
+                             "wait_any_frac": c.get('wait_any_frac')}
         step_bytes = core_bytes(spec) + obs_bytes  # C3: 415 + 10,976 = ALGO_BYTES_PER_ENV_STEP
         pipe_bytes = step_bytes * B * k_call
         if dom:
@@ -292,23 +349,30 @@ def main():
             roof["frac_of_measured"] = round(roof["achieved"] / peak_meas, 5)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))
+            visible = len(os.sched_getaffinity(0))
+            workers = args.cpu_workers or min(BOX_CPU_SHARE, visible)
             v, n, wall = cpu_baseline(args.config, args.cpu_seconds, workers, 12345)
             cpu = {"value": round(v, 1), "unit": "env-steps/s", "cores": workers, "kind": "port",
+                   "per_core": round(v / workers, 1),
+                   "all_visible_cores_linear": round(v / workers * visible, 1),
                    "sample": f"{n} env-steps of {args.config} (obs incl., auto-reset) on {workers} processes x "
-                             f"{wall:.1f}s, C restatement oracle/mfg_oracle.c, 1 env per process, "
-                             f"{len(os.sched_getaffinity(0))} cores visible, {cpu_model()}"}
+                             f"{wall:.1f}s, C restatement oracle/mfg_oracle.c, 1 env per process (independent "
+                             f"envs: linear in cores); {visible} cores visible, the box allots {BOX_CPU_SHARE} "
+                             f"per GPU; {cpu_model()}"}
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": f"f64 rewards/battery/dirt, {args.obs_dtype} obs",
             "data": "synthetic (Philox4x32-10 uniform random actions, device-side)",
             "config": {"workload": f"C3 {Path(args.config).stem}: 'large' level, 8 agents, doors+items+batteries, "
                                    f"pomdp_r 3" if args.config == 'large8.yaml' else Path(args.config).stem,
-                       "envs_per_gpu": B, "global_batch": B * world, "obs": "dense fp32 per env-step",
+                       "envs_per_gpu": B, "global_batch": B * world,
+                       "obs": f"dense {args.obs_dtype} per env-step ({obs_bytes} B)",
                        "fuse": F, "auto_reset": True, "parallelism": f"env-shard x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "alt_obs_dtype": alt,
         }
         print(json.dumps(out))
     eng.close()

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MFG_ABI_VERSION 1
+#define MFG_ABI_VERSION 2
 
 #define MFG_MAX_AGENTS 64
 #define MFG_MAX_ACTIONS 16
@@ -153,25 +153,65 @@ typedef struct mfg_spec {
   uint32_t env_seed;
 } mfg_spec;
 
-/* Per env-step event record: everything the reference's info dict is built from (results.py:42-84,
- * factory.py:222-259). The host rebuilds the exact dict from (actions, events, spec). */
+/* ---- per env-step event rows written by mfg_step (the info dict is rebuilt from them) ----
+ * ev_act   u8 [K][B][A]: bit0 action valid, bit1 action_introduced_collision (results.py:62-84),
+ *                        bit2 ItemAction took the drop-off branch (items/actions.py:43-52), bit7 the agent acted
+ * ev_watch u8 [K][B][A]: bit0 WatchCollisions result (rules.py:276-307), bit1 battery discharged at post-step
+ *                        (batteries/rules.py:66-87), bit2 DoneAtMaintainerCollision result (maintenance/rules.py:32-40),
+ *                        bits3..7 number of destinations this agent was credited with by the reach rule
+ *                        (destinations/rules.py:34-54; TickResult entity = the agent)
+ * ev_misc i32 [K][B][MFG_EV_MISC_N]: slots MFG_EVM_* below. */
+#define MFG_EV_MISC_N 12
+enum {
+  MFG_EVM_DOOR_COLL_LO = 0,  /* doors (bit d) that received a WatchCollisions result, bits 0..31 */
+  MFG_EVM_DOOR_COLL_HI = 1,  /* ... doors 32..63 */
+  MFG_EVM_RESPAWN_ITEMS = 2, /* RespawnItems result value, -1 = no result this step (items/rules.py:35-43) */
+  MFG_EVM_DIRT_SPAWN = 3,    /* RespawnDirt result value, -1 = no result (clean_up/rules.py:49-59) */
+  MFG_EVM_DIRT_VALID = 4,    /* ... and its validity */
+  MFG_EVM_DEST_REACHED = 5,  /* destinations marked reached this step (sum of ev_watch bits 3..7) */
+  MFG_EVM_FLAGS = 6,         /* bit0 DoorAutoClose emitted its result, bit1 crashed, bits 8..15 crash reason (MFG_CRASH_*) */
+  MFG_EVM_DONE_MASK = 7,     /* bit r: rule r produced a VALID DoneResult; bit 31: WatchCollisions done */
+  MFG_EVM_STEP = 8,          /* Gamestate.curr_step after the step (the info dict's 'step') */
+  MFG_EVM_EPISODE = 9,       /* resets done so far */
+  MFG_EVM_MAINT_COLL = 10,   /* maintainers (collection slot bit) that received a WatchCollisions result */
+  MFG_EVM_MAINT_BASE = 11    /* u_int of the first maintainer: names are 'Maintainer[base + slot]' */
+};
+
+/* Crash reasons (reference crash paths; engine capacity). A crashed env reports done = 1. */
+enum {
+  MFG_CRASH_NONE = 0,
+  MFG_CRASH_RULE = 1,        /* DestAction on a destination (AttributeError, Q17) or the RespawnItems TypeError (Q9) */
+  MFG_CRASH_ROUTE = 2,       /* maintainer route: NodeNotFound / NetworkXNoPath */
+  MFG_CRASH_NO_FREE = 3,     /* maintainer random_free_position on a full level (IndexError) */
+  MFG_CRASH_NEXT_EMPTY = 4,  /* maintainer pops from an empty target list */
+  MFG_CRASH_PATH_EMPTY = 5,  /* maintainer reads self._path[0] of an empty path */
+  MFG_CRASH_MOVE = 6,        /* maintainer step not in MOVEMAP */
+  MFG_CRASH_CAPACITY = 7,    /* engine capacity exceeded (dirt slots, id-pair list, reach counter) */
+  MFG_CRASH_ACTION = 8       /* action index outside [0, n_actions[a]) (IndexError upstream, factory.py:201-206) */
+};
+
+/* Decoded form of one env-step's event rows (host side; the oracle reports the same record). */
 typedef struct mfg_events {
-  uint8_t act[MFG_MAX_AGENTS];       /* bit0 action valid, bit1 action_introduced_collision,
-                                        bit2 ItemAction took the drop-off branch, bit7 acted */
-  uint8_t watch[MFG_MAX_AGENTS];     /* bit0 WatchCollisions result, bit1 battery discharged at post-step,
-                                        bit2 DoneAtMaintainerCollision result for this agent */
-  uint64_t door_coll;                /* doors that received a WatchCollisions result */
-  uint64_t maint_coll;               /* maintainers that received a WatchCollisions result */
-  int32_t respawn_items_value;       /* RespawnItems result value, -1 = no result this step */
-  int32_t dirt_spawn_value;          /* RespawnDirt result value, -1 = no result */
-  int32_t dirt_spawn_valid;
-  int32_t dest_reach_agent[4];       /* agent index credited by DestinationReachReward per destination, -1 none */
-  int32_t door_autoclose;            /* DoorAutoClose emitted its result */
-  int32_t done_mask;                 /* bit r: rule r produced a VALID DoneResult */
-  int32_t crashed;                   /* reference crash path hit (Q17): env flagged, done */
-  int32_t step;
-  int32_t maint_base;                /* u_int of the first maintainer (names 'Maintainer[maint_base + k]') */
+  uint8_t act[MFG_MAX_AGENTS];       /* ev_act row */
+  uint8_t watch[MFG_MAX_AGENTS];     /* ev_watch row */
+  uint64_t door_coll;                /* MFG_EVM_DOOR_COLL_LO | HI << 32 */
+  uint64_t maint_coll;               /* MFG_EVM_MAINT_COLL */
+  int32_t respawn_items_value;       /* MFG_EVM_RESPAWN_ITEMS */
+  int32_t dirt_spawn_value;          /* MFG_EVM_DIRT_SPAWN */
+  int32_t dirt_spawn_valid;          /* MFG_EVM_DIRT_VALID */
+  int32_t dest_reached;              /* MFG_EVM_DEST_REACHED */
+  int32_t door_autoclose;            /* MFG_EVM_FLAGS bit0 */
+  int32_t done_mask;                 /* MFG_EVM_DONE_MASK */
+  int32_t crashed;                   /* MFG_EVM_FLAGS bit1 */
+  int32_t crash_reason;              /* MFG_EVM_FLAGS bits 8..15 */
+  int32_t step;                      /* MFG_EVM_STEP */
+  int32_t episode;                   /* MFG_EVM_EPISODE */
+  int32_t maint_base;                /* MFG_EVM_MAINT_BASE */
 } mfg_events;
+
+/* Decode one env's rows (ev_act/ev_watch: n_agents bytes, ev_misc: MFG_EV_MISC_N ints, all host memory). */
+int mfg_decode_events(const uint8_t* ev_act, const uint8_t* ev_watch, const int32_t* ev_misc, int n_agents,
+                      mfg_events* out);
 
 /* ---- engine ABI (HIP) ---- */
 typedef struct mfg_engine mfg_engine;
@@ -180,10 +220,14 @@ typedef struct mfg_engine mfg_engine;
 int mfg_abi_version(void);
 
 /* Create B = n_envs environments of `spec` on HIP device `device`. Replaces Factory.__init__
- * (factory.py:81-129) for a whole batch; no env is initialised until mfg_reset(init=1). */
+ * (factory.py:81-129) for a whole batch; no env is initialised until mfg_reset(init=1). Every bounded spec
+ * count is validated (returns < 0 instead of reading out of bounds). The caller's current HIP device is
+ * restored before any entry point returns; the engine's calls always run on `device`. */
 int mfg_create(const mfg_spec* spec, int device, int64_t n_envs, mfg_engine** out);
 int mfg_destroy(mfg_engine* e);
-const char* mfg_last_error(void);
+/* Message of the last failed call on engine e (per engine); e == NULL: the calling thread's last failed
+ * mfg_create / argument check. Valid until the next call on the same engine (or thread). */
+const char* mfg_last_error(const mfg_engine* e);
 
 /* Reset envs (mask[b] != 0, or all if mask == NULL); Factory.reset (factory.py:134-148).
  * init = 0: reset existing envs. init & MFG_INIT_CREATE: first create the envs (Factory.__init__,
@@ -199,8 +243,10 @@ int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int 
 /* K fused env-steps of every env; Factory.step (factory.py:189-220) + auto-reset.
  * actions: device int32 [K][B][A] indices into each agent's action list, or NULL for synthetic uniform
  * actions from Philox4x32-10 keyed (philox_seed, env_base + b) at counter (step_base + k, agent).
- * Outputs (device, each may be NULL): reward f64 [K][B][A], done u8 [K][B], obs [K][B][A][lmax][d][d],
- * ev_act / ev_watch u8 [K][B][A] and ev_misc i32 [K][B][10] (the info-dict event record).
+ * Outputs (device, each may be NULL): reward f64 [K][B][A], done u8 [K][B], obs [K][B][A][lmax][h][w]
+ * (h = w = 2 pomdp_r + 1, or the level's H x W when pomdp_r == 0), ev_act / ev_watch u8 [K][B][A] and
+ * ev_misc i32 [K][B][MFG_EV_MISC_N] (the info-dict event rows above).
+ * An action index outside [0, n_actions[a]) crashes that env (MFG_CRASH_ACTION, done = 1).
  * auto_reset != 0: an env whose step is done is reset before its obs row is rendered, so the row is the
  * new episode's first observation. Per step the engine launches k_logic, k_resetdone (auto_reset) and
  * k_obs (obs != NULL); pending floor-shuffle debt is replayed (mfg_replay) once before returning. */

@@ -942,7 +942,7 @@ struct StepOut {
   int my_watch_ev;    // lane a: watch event bits
   uint64_t door_coll;
   uint32_t maint_coll;  // maintainers (collection slots) that received a WatchCollisions result
-  int respawn_items_value, dirt_spawn_value, dirt_spawn_valid, door_autoclose, done_mask, dest_pack, crashed;
+  int respawn_items_value, dirt_spawn_value, dirt_spawn_valid, door_autoclose, done_mask, dest_reached, crashed;
   int done;
 };
 
@@ -1480,8 +1480,12 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
       if (e.lane == 0) e.dests()[i] = w | EW_REACHED;
       wave_sync();
       add_agent_reward(e, o, last, ru.f[0]);
-      for (int k = 0; k < 4; k++)
-        if (((o.dest_pack >> (8 * k)) & 0xFF) == 0) { o.dest_pack |= (last + 1) << (8 * k); break; }
+      // info: one '<agent>_<rule>' entry per credited destination; count per agent in ev_watch bits 3..7
+      if (e.lane == last) {
+        if (o.my_watch_ev >= (31 << 3)) e.hdr()[H_OVERFLOW] = 1;
+        else o.my_watch_ev += 1 << 3;
+      }
+      o.dest_reached++;
     }
   }
 }
@@ -2180,7 +2184,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
 // ------------------------------------------------------------------------------------------------
 // one env-step (Factory.step, factory.py:189-220; Gamestate.tick, states.py:170-203)
 // ------------------------------------------------------------------------------------------------
-#define MFG_EV_MISC 12
+#define MFG_EV_MISC MFG_EV_MISC_N
 
 template <bool RNG, bool MAINT>
 __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
@@ -2188,13 +2192,14 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   const int A = S->A;
   o.my_rew = 0.0; o.g_rew = 0.0; o.my_act_ev = 0; o.my_watch_ev = 0; o.door_coll = 0; o.maint_coll = 0;
   o.respawn_items_value = -1; o.dirt_spawn_value = -1; o.dirt_spawn_valid = 0; o.door_autoclose = 0;
-  o.done_mask = 0; o.dest_pack = 0; o.crashed = 0; o.done = 0;
+  o.done_mask = 0; o.dest_reached = 0; o.crashed = 0; o.done = 0;
   e.setH(H_STEP, e.H(H_STEP) + 1);
   e.setH(H_TOTAL_STEPS, e.H(H_TOTAL_STEPS) + 1);
   wave_sync();
   for (int a = 0; a < A && !o.crashed; a++) {
     if (uni(e.agpar()[a])) continue;  // paralyzed agents skip their action
     const int slot = rl(my_act, a);
+    if (slot < 0 || slot >= S->s.n_actions[a]) { o.crashed = MFG_CRASH_ACTION; break; }  // IndexError upstream
     do_action(e, o, a, slot);
   }
   const int nr = S->s.n_rules;
@@ -2206,9 +2211,9 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
     for (int r = 0; r < nr; r++) rule_check_done(e, o, r);
   // the step's membership-only shuffles stay as debt: paid by k_replay after the launch, or inline by
   // the next order-dependent consumer (spawn / reset)
-  if (o.crashed || e.H(H_OVERFLOW)) {  // H_CRASHED keeps the reason: 1 rule/action crash upstream, 2-6 maintainer
-    e.setH(H_CRASHED, o.crashed ? o.crashed : 7);  // (route, free cell, next, path, move), 7 capacity overflow
-    o.crashed = 1;
+  if (o.crashed || e.H(H_OVERFLOW)) {  // H_CRASHED keeps the reason (MFG_CRASH_*, include/mfg.h)
+    o.crashed = o.crashed ? o.crashed : MFG_CRASH_CAPACITY;
+    e.setH(H_CRASHED, o.crashed);
     o.done = 1;
   }
   wave_sync();
@@ -2232,8 +2237,8 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
       m[2] = o.respawn_items_value;
       m[3] = o.dirt_spawn_value;
       m[4] = o.dirt_spawn_valid;
-      m[5] = o.dest_pack;
-      m[6] = (o.door_autoclose ? 1 : 0) | (o.crashed ? 2 : 0);
+      m[5] = o.dest_reached;
+      m[6] = (o.door_autoclose ? 1 : 0) | (o.crashed ? 2 : 0) | ((o.crashed & 0xFF) << 8);
       m[7] = o.done_mask;
       m[8] = e.hdr()[H_STEP];
       m[9] = e.hdr()[H_EPISODE];
@@ -2487,6 +2492,7 @@ struct mfg_engine {
   std::vector<hipEvent_t> ev_free;
   struct Mark { int k; hipEvent_t a, b; };
   std::vector<Mark> marks;
+  std::string err;  // mfg_last_error(e)
 };
 
 static hipEvent_t prof_event(mfg_engine* e) {
@@ -2514,7 +2520,52 @@ static int fail(const std::string& m) {
     if (_e != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-extern "C" const char* mfg_last_error(void) { return g_err.c_str(); }
+extern "C" const char* mfg_last_error(const mfg_engine* e) { return e ? e->err.c_str() : g_err.c_str(); }
+
+// Entry points run on the engine's device and give the caller's current device back (mfg.h, mfg_create).
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DevGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+// run an engine entry point on its device; a failure's message is kept per engine
+#define ENGINE_CALL(E, CALL)                 \
+  do {                                       \
+    if (!(E)) return fail("null engine");    \
+    DevGuard _g((E)->device);                \
+    const int _rc = (CALL);                  \
+    if (_rc) (E)->err = g_err;               \
+    return _rc;                              \
+  } while (0)
+
+extern "C" int mfg_decode_events(const uint8_t* ev_act, const uint8_t* ev_watch, const int32_t* ev_misc, int n_agents,
+                                 mfg_events* out) {
+  if (!ev_act || !ev_watch || !ev_misc || !out) return fail("null argument");
+  if (n_agents < 1 || n_agents > MFG_MAX_AGENTS) return fail("n_agents out of range");
+  memset(out, 0, sizeof(*out));
+  for (int a = 0; a < n_agents; a++) { out->act[a] = ev_act[a]; out->watch[a] = ev_watch[a]; }
+  const int32_t* m = ev_misc;
+  out->door_coll = (uint64_t)(uint32_t)m[MFG_EVM_DOOR_COLL_LO] | ((uint64_t)(uint32_t)m[MFG_EVM_DOOR_COLL_HI] << 32);
+  out->maint_coll = (uint64_t)(uint32_t)m[MFG_EVM_MAINT_COLL];
+  out->respawn_items_value = m[MFG_EVM_RESPAWN_ITEMS];
+  out->dirt_spawn_value = m[MFG_EVM_DIRT_SPAWN];
+  out->dirt_spawn_valid = m[MFG_EVM_DIRT_VALID];
+  out->dest_reached = m[MFG_EVM_DEST_REACHED];
+  out->door_autoclose = m[MFG_EVM_FLAGS] & 1;
+  out->crashed = (m[MFG_EVM_FLAGS] >> 1) & 1;
+  out->crash_reason = (m[MFG_EVM_FLAGS] >> 8) & 0xFF;
+  out->done_mask = m[MFG_EVM_DONE_MASK];
+  out->step = m[MFG_EVM_STEP];
+  out->episode = m[MFG_EVM_EPISODE];
+  out->maint_base = m[MFG_EVM_MAINT_BASE];
+  return 0;
+}
 
 template <typename T>
 static int upload(mfg_engine* e, const T* src, size_t n, const T** dst) {
@@ -2659,13 +2710,62 @@ static int probe_xchg_order(int device) {
   return h == 0 ? 1 : 0;
 }
 
+// every bounded count of a caller-built spec (the kernels index fixed-size spec arrays with them)
+static int validate_spec(const mfg_spec* s) {
+  if (s->abi_version != MFG_ABI_VERSION) return fail("spec ABI version mismatch");
+  if (s->H < 1 || s->W < 1 || !s->level) return fail("empty level");
+  if (s->H * s->W > 65535) return fail("level too large for 16-bit cell indices");
+  if (s->n_agents < 1 || s->n_agents > MFG_MAX_AGENTS) return fail("n_agents out of range");
+  if (s->n_doors < 0 || s->n_doors > MFG_MAX_DOORS) return fail("too many doors");
+  if (s->n_floor < 1 || s->n_floor > s->H * s->W || !s->floor_cells) return fail("n_floor out of range");
+  if (s->n_walls < 0 || s->n_walls > s->H * s->W) return fail("n_walls out of range");
+  if (s->pomdp_r < 1 || s->pomdp_r > 8) return fail("engine supports pomdp_r in [1,8]");
+  if (s->n_rays < 1 || !s->ray_off || !s->ray_pts) return fail("empty ray table");
+  if (s->n_rules < 0 || s->n_rules > MFG_MAX_RULES) return fail("n_rules out of range");
+  for (int a = 0; a < s->n_agents; a++) {
+    if (s->n_actions[a] < 1 || s->n_actions[a] > MFG_MAX_ACTIONS) return fail("n_actions out of range");
+    if (s->n_layers[a] < 0 || s->n_layers[a] > MFG_MAX_LAYERS) return fail("n_layers out of range");
+    if (s->combined_n[a] < 0 || s->combined_n[a] > MFG_MAX_COMBINED) return fail("combined_n out of range");
+    for (int j = 0; j < s->n_actions[a]; j++) {
+      const mfg_action& ac = s->actions[a][j];
+      if (ac.op < MFG_ACT_NOOP || ac.op > MFG_ACT_MACHINE) return fail("unknown action opcode");
+      if (ac.op == MFG_ACT_MOVE && (ac.arg < 0 || ac.arg > 7)) return fail("move direction out of range");
+    }
+    for (int l = 0; l < s->n_layers[a]; l++) {
+      const int k = s->layers[a][l].kind, t = s->layers[a][l].tag;
+      if (k < MFG_LAYER_ZERO || k > MFG_LAYER_GLOBALPOS) return fail("unknown layer kind");
+      if (k == MFG_LAYER_TAG && !((t >= 0 && t <= MFG_TAG_MAINTAINERS) ||
+                                  (t >= MFG_TAG_AGENT0 && t < MFG_TAG_AGENT0 + s->n_agents)))
+        return fail("layer tag out of range");
+    }
+    for (int q = 0; q < s->combined_n[a]; q++) {
+      const int t = s->combined_tags[a][q];
+      if (!((t >= 0 && t <= MFG_TAG_MAINTAINERS) || (t >= MFG_TAG_AGENT0 && t < MFG_TAG_AGENT0 + s->n_agents)))
+        return fail("combined tag out of range");
+    }
+  }
+  for (int r = 0; r < s->n_rules; r++)
+    if (s->rules[r].op < MFG_RULE_SPAWN_BATTERIES || s->rules[r].op > MFG_RULE_DONE_MAINT_COLLISION)
+      return fail("unknown rule opcode");
+  for (int f = 0; f < s->n_floor; f++)
+    if (s->floor_cells[f] < 0 || s->floor_cells[f] >= s->H * s->W) return fail("floor cell out of range");
+  for (int w = 0; w < s->n_walls; w++)
+    if (!s->wall_cells || s->wall_cells[w] < 0 || s->wall_cells[w] >= s->H * s->W) return fail("wall cell out of range");
+  for (int d = 0; d < s->n_doors; d++)
+    if (!s->door_cells || s->door_cells[d] < 0 || s->door_cells[d] >= s->H * s->W) return fail("door cell out of range");
+  return 0;
+}
+
+static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out);
 extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out) {
   if (!s || !out) return fail("null argument");
-  if (s->abi_version != MFG_ABI_VERSION) return fail("spec ABI version mismatch");
-  if (s->n_agents < 1 || s->n_agents > MFG_MAX_AGENTS) return fail("n_agents out of range");
-  if (s->n_doors > MFG_MAX_DOORS) return fail("too many doors");
-  if (s->pomdp_r < 1 || s->pomdp_r > 8) return fail("engine supports pomdp_r in [1,8]");
-  if (s->H * s->W > 65535) return fail("level too large for 16-bit cell indices");
+  if (n_envs < 1) return fail("n_envs must be >= 1");
+  if (validate_spec(s)) return -1;
+  DevGuard g(device);
+  return create_impl(s, device, n_envs, out);
+}
+
+static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out) {
   auto* e = new mfg_engine();
   e->device = device;
   e->B = n_envs;
@@ -2904,7 +3004,7 @@ extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_eng
 
 extern "C" int mfg_destroy(mfg_engine* e) {
   if (!e) return 0;
-  (void)hipSetDevice(e->device);
+  DevGuard g(e->device);
   for (void* p : e->d_bufs) (void)hipFree(p);
   if (e->d_spec) (void)hipFree(e->d_spec);
   if (e->d_state) (void)hipFree(e->d_state);
@@ -2977,9 +3077,15 @@ static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st) {
 
 // reset (init=1: create envs, seeding env i with random.seed(seed_base + i)); obs_dtype 0=f32 1=f64.
 // With a mask only the masked envs are reset, but obs (if given) is rendered for every env.
+static int reset_impl(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init, uint64_t seed_base,
+                      void* stream);
 extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init,
                          uint64_t seed_base, void* stream) {
-  if (!e) return fail("null engine");
+  ENGINE_CALL(e, reset_impl(e, mask, obs, obs_dtype, init, seed_base, stream));
+}
+static int reset_impl(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init, uint64_t seed_base,
+                      void* stream) {
+  if (obs_dtype != 0 && obs_dtype != 1) return fail("obs_dtype must be 0 (f32) or 1 (f64)");
   hipStream_t st = (hipStream_t)stream;
   PROF_BEGIN(e, st);
   hipLaunchKernelGGL(k_reset, GEOM(e->h.lds_full), st, e->d_spec,
@@ -2991,8 +3097,9 @@ extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_
 }
 
 // Pay all pending floor-shuffle debt (membership-only shuffles of the reference's move checks, Q3).
-extern "C" int mfg_replay(mfg_engine* e, void* stream) {
-  if (!e) return fail("null engine");
+static int replay_impl(mfg_engine* e, void* stream);
+extern "C" int mfg_replay(mfg_engine* e, void* stream) { ENGINE_CALL(e, replay_impl(e, stream)); }
+static int replay_impl(mfg_engine* e, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   PROF_BEGIN(e, st);
   hipLaunchKernelGGL(k_replay, GEOM(e->h.lds_replay_per_wave), st, e->d_spec, e->d_state,
@@ -3009,11 +3116,20 @@ extern "C" int mfg_replay(mfg_engine* e, void* stream) {
 // ev_misc [K][B][10] i32. auto_reset: envs that finish are reset (the obs row is then the first
 // observation of the new episode). Per step: k_logic, k_resetdone (auto_reset), k_obs (obs); then one
 // k_replay for the whole call.
+static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
+                     int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
+                     uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream);
 extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
                         int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype,
                         uint8_t* ev_act, uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
-  if (!e) return fail("null engine");
+  ENGINE_CALL(e, step_impl(e, K, actions, philox_seed, env_base, step_base, reward, done, obs, obs_dtype, ev_act,
+                           ev_watch, ev_misc, auto_reset, stream));
+}
+static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
+                     int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
+                     uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
   if (K < 1) return fail("K must be >= 1");
+  if (obs && obs_dtype != 0 && obs_dtype != 1) return fail("obs_dtype must be 0 (f32) or 1 (f64)");
   hipStream_t st = (hipStream_t)stream;
   const size_t B = (size_t)e->B, A = (size_t)e->h.A;
   const size_t obs_row = B * A * (size_t)e->h.obs_agent_stride * (obs_dtype == 1 ? 8 : 4);
@@ -3059,19 +3175,20 @@ extern "C" int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t p
     if (obs && launch_obs(e, (uint8_t*)obs + (size_t)k * obs_row, obs_dtype, st)) return -1;
 #endif
   }
-  return mfg_replay(e, stream);
+  return replay_impl(e, stream);
 }
 
 // snapshots (checkpoints == fixtures): whole state buffer device<->device, B * layout.size bytes
-extern "C" int mfg_export_state(mfg_engine* e, void* dst, void* stream) {
-  if (!e || !dst) return fail("null argument");
-  HIPCHK(hipMemcpyAsync(dst, e->d_state, (size_t)e->h.L.size * e->B, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+static int copy_state(mfg_engine* e, void* dst, const void* src, void* stream) {
+  if (!dst || !src) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(dst, src, (size_t)e->h.L.size * e->B, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
 }
+extern "C" int mfg_export_state(mfg_engine* e, void* dst, void* stream) {
+  ENGINE_CALL(e, copy_state(e, dst, e->d_state, stream));
+}
 extern "C" int mfg_import_state(mfg_engine* e, const void* src, void* stream) {
-  if (!e || !src) return fail("null argument");
-  HIPCHK(hipMemcpyAsync(e->d_state, src, (size_t)e->h.L.size * e->B, hipMemcpyDeviceToDevice, (hipStream_t)stream));
-  return 0;
+  ENGINE_CALL(e, copy_state(e, e->d_state, src, stream));
 }
 extern "C" int mfg_profile(mfg_engine* e, int enable) {
   if (!e) return fail("null engine");
@@ -3079,8 +3196,12 @@ extern "C" int mfg_profile(mfg_engine* e, int enable) {
   return 0;
 }
 
+static int profile_read_impl(mfg_engine* e, double* total_ms, int64_t* launches, int n);
 extern "C" int mfg_profile_read(mfg_engine* e, double* total_ms, int64_t* launches, int n) {
-  if (!e || !total_ms || !launches) return fail("null argument");
+  ENGINE_CALL(e, profile_read_impl(e, total_ms, launches, n));
+}
+static int profile_read_impl(mfg_engine* e, double* total_ms, int64_t* launches, int n) {
+  if (!total_ms || !launches) return fail("null argument");
   for (int k = 0; k < n; k++) { total_ms[k] = 0.0; launches[k] = 0; }
   if (!e->marks.empty()) HIPCHK(hipEventSynchronize(e->marks.back().b));
   for (const auto& m : e->marks) {

@@ -31,6 +31,17 @@ LAYER_ZERO, LAYER_TAG, LAYER_COMBINED, LAYER_BATTERY, LAYER_GLOBALPOS = range(5)
 
 DEST_ANY, DEST_ALL, DEST_SIMULTANEOUS = range(3)
 
+ABI_VERSION = 2
+# ev_misc row (include/mfg.h MFG_EVM_*)
+EV_MISC_N = 12
+(EVM_DOOR_COLL_LO, EVM_DOOR_COLL_HI, EVM_RESPAWN_ITEMS, EVM_DIRT_SPAWN, EVM_DIRT_VALID, EVM_DEST_REACHED, EVM_FLAGS,
+ EVM_DONE_MASK, EVM_STEP, EVM_EPISODE, EVM_MAINT_COLL, EVM_MAINT_BASE) = range(EV_MISC_N)
+# crash reasons (MFG_CRASH_*)
+CRASH_NAMES = {0: 'none', 1: 'reference crash path (DestAction on a destination Q17 / RespawnItems Q9)',
+               2: 'maintainer route: no path', 3: 'maintainer: no free cell', 4: 'maintainer: empty target list',
+               5: 'maintainer: empty path', 6: 'maintainer: step not in MOVEMAP', 7: 'engine capacity exceeded',
+               8: 'action index out of range'}
+
 
 class MfgAction(C.Structure):
     _fields_ = [('op', C.c_int32), ('arg', C.c_int32), ('valid_reward', C.c_double), ('fail_reward', C.c_double),
@@ -95,10 +106,12 @@ class MfgEvents(C.Structure):
         ('respawn_items_value', C.c_int32),
         ('dirt_spawn_value', C.c_int32),
         ('dirt_spawn_valid', C.c_int32),
-        ('dest_reach_agent', C.c_int32 * 4),
+        ('dest_reached', C.c_int32),
         ('door_autoclose', C.c_int32),
         ('done_mask', C.c_int32),
         ('crashed', C.c_int32),
+        ('crash_reason', C.c_int32),
         ('step', C.c_int32),
+        ('episode', C.c_int32),
         ('maint_base', C.c_int32),
     ]

@@ -13,7 +13,7 @@ import numpy as np
 from . import abi
 
 LIB_PATH = Path(os.environ.get('MFG_HIP_LIB') or Path(__file__).resolve().parent / '_lib' / 'libmfg_hip.so')
-EV_MISC = 12
+EV_MISC = abi.EV_MISC_N  # MFG_EV_MISC_N (include/mfg.h)
 HDR_N = 40  # MFG_HDR_N (csrc/mfg_device.h)
 KERNELS = ['k_logic', 'k_resetdone', 'k_obs', 'k_replay', 'k_reset']  # MFG_K_* ids (include/mfg.h)
 
@@ -44,7 +44,10 @@ def load_lib():
     L.mfg_create.restype = C.c_int
     L.mfg_destroy.argtypes = [C.c_void_p]
     L.mfg_destroy.restype = C.c_int
+    L.mfg_last_error.argtypes = [C.c_void_p]
     L.mfg_last_error.restype = C.c_char_p
+    L.mfg_decode_events.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.mfg_decode_events.restype = C.c_int
     L.mfg_layout.argtypes = [C.c_void_p, C.c_void_p]
     L.mfg_layout.restype = C.c_int
     L.mfg_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_void_p]
@@ -66,7 +69,7 @@ def load_lib():
     L.mfg_profile_read.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     L.mfg_profile_read.restype = C.c_int
     L.mfg_abi_version.restype = C.c_int
-    if L.mfg_abi_version() != 1:
+    if L.mfg_abi_version() != abi.ABI_VERSION:
         raise RuntimeError('libmfg_hip.so ABI version mismatch')
     _lib = L
     return L
@@ -76,9 +79,9 @@ def _ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
-def _check(rc, what):
+def _check(rc, what, h=None):
     if rc != 0:
-        raise RuntimeError(f'{what} failed: {load_lib().mfg_last_error().decode()}')
+        raise RuntimeError(f'{what} failed: {load_lib().mfg_last_error(h).decode()}')
 
 
 class Engine:
@@ -125,14 +128,15 @@ class Engine:
     def reset(self, obs=None, mask=None, init=False, seed_base=0):
         dt = 1 if (obs is not None and obs.dtype == self.torch.float64) else 0
         _check(self.L.mfg_reset(self.h, _ptr(mask), _ptr(obs), dt, int(init), int(seed_base), self._stream()),
-               'mfg_reset')
+               'mfg_reset', self.h)
 
     def step(self, K=1, actions=None, philox_seed=0, env_base=0, step_base=0, reward=None, done=None, obs=None,
              ev_act=None, ev_watch=None, ev_misc=None, auto_reset=True):
         dt = 1 if (obs is not None and obs.dtype == self.torch.float64) else 0
         _check(self.L.mfg_step(self.h, int(K), _ptr(actions), int(philox_seed) & 0xFFFFFFFF, int(env_base),
                                int(step_base), _ptr(reward), _ptr(done), _ptr(obs), dt, _ptr(ev_act),
-                               _ptr(ev_watch), _ptr(ev_misc), int(bool(auto_reset)), self._stream()), 'mfg_step')
+                               _ptr(ev_watch), _ptr(ev_misc), int(bool(auto_reset)), self._stream()), 'mfg_step',
+               self.h)
 
     def profile(self, enable=True):
         """Record HIP events around every kernel launch (on the launch stream) while enabled."""
@@ -205,11 +209,17 @@ class RecordView:
 
 
 def events_from_rows(ev_act, ev_watch, ev_misc):
-    """One env-step's device event rows -> dict in the MfgEvents layout used by info.rebuild_info."""
-    m = [int(x) for x in ev_misc]
-    dest = [((m[5] >> (8 * k)) & 0xFF) - 1 for k in range(4)]
-    return dict(act=[int(x) for x in ev_act], watch=[int(x) for x in ev_watch],
-                door_coll=(m[0] & 0xFFFFFFFF) | ((m[1] & 0xFFFFFFFF) << 32), maint_coll=m[10] & 0xFFFFFFFF,
-                respawn_items_value=m[2], dirt_spawn_value=m[3], dirt_spawn_valid=m[4],
-                dest_reach_agent=dest, door_autoclose=m[6] & 1, crashed=(m[6] >> 1) & 1, done_mask=m[7],
-                step=m[8], maint_base=m[11])
+    """One env-step's device event rows -> dict with the mfg_events fields (include/mfg.h), decoded by the
+    library's own mfg_decode_events so the host and the C-ABI share one row contract."""
+    L = load_lib()
+    act = np.ascontiguousarray(ev_act, np.uint8)
+    watch = np.ascontiguousarray(ev_watch, np.uint8)
+    misc = np.ascontiguousarray(ev_misc, np.int32)
+    assert misc.size == abi.EV_MISC_N and act.size == watch.size
+    ev = abi.MfgEvents()
+    _check(L.mfg_decode_events(act.ctypes.data, watch.ctypes.data, misc.ctypes.data, int(act.size), C.byref(ev)),
+           'mfg_decode_events')
+    out = {k: getattr(ev, k) for k, _ in abi.MfgEvents._fields_}
+    out['act'] = [int(x) for x in act]
+    out['watch'] = [int(x) for x in watch]
+    return out

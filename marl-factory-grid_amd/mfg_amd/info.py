@@ -32,7 +32,7 @@ def rebuild_info(spec, actions, ev, reward):
         if bits & 2:
             info[f'{n}_Collisions'] += 1
     # 2) tick_step results in rule order
-    dest_agents = [x for x in g('dest_reach_agent') if x >= 0]
+    dest_count = [(w >> 3) & 31 for w in watch]  # destinations credited per agent (ev_watch bits 3..7)
     for ri, (op, ri_, rf) in enumerate(spec.rules):
         rname = spec.rule_names[ri]
         if op == abi.RULE_DOOR_AUTOCLOSE and g('door_autoclose'):
@@ -43,9 +43,10 @@ def rebuild_info(spec, actions, ev, reward):
         elif op == abi.RULE_RESPAWN_DIRT and g('dirt_spawn_value') >= 0:
             info['Global_DirtPiles_spawn'] += g('dirt_spawn_value')
         elif op in (abi.RULE_DEST_REACH, abi.RULE_DONE_DEST):
-            for a in dest_agents:
-                info[f'{names[a]}_{rname}'] += rf[0]
-            dest_agents = []  # a second reach rule sees every destination already marked
+            for a, n in enumerate(names):
+                for _ in range(dest_count[a]):
+                    info[f'{n}_{rname}'] += rf[0]
+            dest_count = [0] * len(names)  # a second reach rule sees every destination already marked
     # 3) tick_post_step results in rule order
     for ri, (op, ri_, rf) in enumerate(spec.rules):
         rname = spec.rule_names[ri]

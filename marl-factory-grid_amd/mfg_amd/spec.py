@@ -460,7 +460,7 @@ def _ptr(arr, ctype, keep):
 def _to_c(es: EnvSpec) -> abi.MfgSpec:
     s = abi.MfgSpec()
     k = es._keep
-    s.abi_version = 1
+    s.abi_version = abi.ABI_VERSION
     s.H, s.W = es.H, es.W
     s.level = _ptr(es.level.astype(np.uint8), C.c_uint8, k)
     s.n_floor = len(es.floor_cells)

@@ -66,7 +66,89 @@ def test_hip_library_exports_every_declared_symbol():
     for f in funcs:
         assert hasattr(lib, f), f'{f} declared in include/mfg.h but not exported'
     lib.mfg_abi_version.restype = C.c_int
-    assert lib.mfg_abi_version() == 1
+    assert lib.mfg_abi_version() == 2
+
+
+def _hip_lib():
+    from mfg_amd.engine import LIB_PATH
+    if not LIB_PATH.exists():
+        import __graft_entry__
+        __graft_entry__.build_hip()
+    lib = C.CDLL(str(LIB_PATH))
+    lib.mfg_last_error.argtypes = [C.c_void_p]
+    lib.mfg_last_error.restype = C.c_char_p
+    return lib
+
+
+def _header_enum(prefix):
+    txt = (ROOT / 'include' / 'mfg.h').read_text()
+    out = {m.group(1): int(m.group(2)) for m in re.finditer(rf'\b({prefix}[A-Z0-9_]+)\s*=\s*(\d+)', txt)}
+    out.update({m.group(1): int(m.group(2)) for m in re.finditer(rf'#define\s+({prefix}[A-Z0-9_]+)\s+(\d+)', txt)})
+    return out
+
+
+def test_event_row_contract_matches_header():
+    """The ev_misc row width and slot numbers of include/mfg.h are the ones the host decodes with."""
+    from mfg_amd import abi
+    from mfg_amd.engine import EV_MISC
+    h = _header_enum('MFG_EV')
+    assert h['MFG_EV_MISC_N'] == abi.EV_MISC_N == EV_MISC == 12
+    for k, v in h.items():
+        if k.startswith('MFG_EVM_'):
+            assert getattr(abi, k[4:]) == v, k
+    crash = _header_enum('MFG_CRASH_')
+    assert sorted(crash.values()) == sorted(abi.CRASH_NAMES)
+
+
+def test_decode_events_through_the_abi():
+    """mfg_decode_events (pure host code) decodes every slot of a row triple; events_from_rows uses it."""
+    from mfg_amd import abi
+    from mfg_amd.engine import events_from_rows
+    A = 5
+    act = np.array([0x81, 0x80, 0x83, 0, 0x85], np.uint8)
+    watch = np.array([1 | (2 << 3), 2, 4, 0, 8], np.uint8)
+    misc = np.zeros(abi.EV_MISC_N, np.int32)
+    misc[abi.EVM_DOOR_COLL_LO] = -2147483647  # bit 0 and bit 31
+    misc[abi.EVM_DOOR_COLL_HI] = 5
+    misc[abi.EVM_RESPAWN_ITEMS] = -1
+    misc[abi.EVM_DIRT_SPAWN] = 3
+    misc[abi.EVM_DIRT_VALID] = 1
+    misc[abi.EVM_DEST_REACHED] = 3
+    misc[abi.EVM_FLAGS] = 1 | 2 | (8 << 8)
+    misc[abi.EVM_DONE_MASK] = -2147483648 | 4
+    misc[abi.EVM_STEP] = 17
+    misc[abi.EVM_EPISODE] = 2
+    misc[abi.EVM_MAINT_COLL] = 6
+    misc[abi.EVM_MAINT_BASE] = 40
+    ev = events_from_rows(act, watch, misc)
+    assert ev['act'] == list(act) and ev['watch'] == list(watch)
+    assert ev['door_coll'] == (1 | (1 << 31) | (5 << 32))
+    assert ev['respawn_items_value'] == -1 and ev['dirt_spawn_value'] == 3 and ev['dirt_spawn_valid'] == 1
+    assert ev['dest_reached'] == 3 and ev['door_autoclose'] == 1 and ev['crashed'] == 1
+    assert ev['crash_reason'] == 8 and ev['done_mask'] == (-2147483648 | 4)
+    assert ev['step'] == 17 and ev['episode'] == 2 and ev['maint_coll'] == 6 and ev['maint_base'] == 40
+
+
+def test_create_validates_spec_without_touching_the_gpu():
+    """Out-of-range spec counts are refused by mfg_create before any HIP call, with a message
+    from mfg_last_error(NULL)."""
+    from mfg_amd.spec import compile_spec
+    lib = _hip_lib()
+    lib.mfg_create.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_void_p)]
+    cases = [('n_actions', lambda c: c.n_actions.__setitem__(0, 17), 'n_actions'),
+             ('n_layers', lambda c: c.n_layers.__setitem__(1, 40), 'n_layers'),
+             ('combined_n', lambda c: c.combined_n.__setitem__(0, 100), 'combined_n'),
+             ('n_rules', lambda c: setattr(c, 'n_rules', 33), 'n_rules'),
+             ('move arg', lambda c: setattr(c.actions[0][4], 'arg', 9), 'direction'),
+             ('layer tag', lambda c: setattr(c.layers[0][2], 'tag', 99), 'tag'),
+             ('abi', lambda c: setattr(c, 'abi_version', 1), 'ABI')]
+    for name, mutate, msg in cases:
+        spec = compile_spec('large8.yaml')
+        mutate(spec.c)
+        h = C.c_void_p()
+        rc = lib.mfg_create(C.byref(spec.c), 0, 4, C.byref(h))
+        assert rc < 0 and not h.value, name
+        assert msg in lib.mfg_last_error(None).decode(), (name, lib.mfg_last_error(None))
 
 
 def test_struct_layouts_agree():
