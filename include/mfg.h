@@ -31,6 +31,7 @@ extern "C" {
 #define MFG_MAX_COMBINED 72
 #define MFG_MAX_RULES 32
 #define MFG_MAX_DOORS 64
+#define MFG_MAX_POSITIONS 16  /* configured spawn / destination cells per agent */
 
 /* ---- action opcodes (reference: environment/actions.py, modules/<m>/actions.py) ---- */
 enum {
@@ -78,7 +79,9 @@ enum {
   MFG_RULE_DOOR_AUTOCLOSE,       /* doors/rules.py:8-28 */
   MFG_RULE_RESPAWN_ITEMS,        /* items/rules.py:9-43: i[0]=n_items i[1]=respawn_freq */
   MFG_RULE_WATCH_COLLISIONS,     /* rules.py:256-325: f[0]=reward i[0]=done_at_collisions f[1]=reward_at_done */
-  MFG_RULE_BATTERY_DECHARGE,     /* batteries/rules.py:9-87: f[0]=per_action_cost f[1]=discharge_reward i[0]=paralyze */
+  MFG_RULE_BATTERY_DECHARGE,     /* batteries/rules.py:9-87: f[0]=per_action_cost f[1]=discharge_reward i[0]=paralyze
+                                    i[2]=per-action cost dict (mfg_action.battery_cost), f[3]=its 'Noop' entry (paralyzed
+                                    agents), i[3]=the dict has 'Noop' */
   MFG_RULE_DONE_BATTERY,         /* batteries/rules.py:90-128: as DECHARGE + i[1]=mode_single f[2]=reward_done */
   MFG_RULE_DONE_MAXSTEPS,        /* rules.py:202-225: i[0]=max_steps */
   MFG_RULE_RESPAWN_DIRT,         /* clean_up/rules.py:28-59: i[0]=freq i[1]=respawn_n f[0]=respawn_amount */
@@ -87,7 +90,10 @@ enum {
   MFG_RULE_DEST_REACH,           /* destinations/rules.py:20-54: f[0]=reward */
   MFG_RULE_DONE_DEST,            /* destinations/rules.py:57-92: f[0]=reach reward f[1]=reward_at_done i[0]=condition */
   MFG_RULE_MOVE_MAINTAINERS,     /* maintenance/rules.py:9-21 */
-  MFG_RULE_DONE_MAINT_COLLISION  /* maintenance/rules.py:24-40 */
+  MFG_RULE_DONE_MAINT_COLLISION, /* maintenance/rules.py:24-40 */
+  MFG_RULE_SPAWN_DEST_ON_AGENT,  /* destinations/rules.py:136-162: one destination bound to each agent, on its cell */
+  MFG_RULE_SPAWN_DEST_PER_AGENT, /* destinations/rules.py:95-133: spec.dest_entry_* (one bound destination per entry) */
+  MFG_RULE_RANDOM_INIT_STEPS     /* rules.py:328-355 DoRandomInitialSteps (on_reset_post_spawn): i[0] = random_steps */
 };
 
 enum { MFG_DEST_ANY = 0, MFG_DEST_ALL = 1, MFG_DEST_SIMULTANEOUS = 2 };
@@ -96,6 +102,8 @@ typedef struct mfg_action {
   int32_t op, arg;
   double valid_reward, fail_reward;
   double aux0, aux1; /* ItemAction: valid / failed drop-off reward */
+  double battery_cost; /* per-action battery cost of a BatteryDecharge rule whose per_action_costs is a dict
+                          (rule i[2] = 1), keyed by the action's class name; NaN = key missing (KeyError) */
 } mfg_action;
 
 typedef struct mfg_layer {
@@ -120,12 +128,15 @@ typedef struct mfg_spec {
   int32_t n_doors;
   const int32_t* door_cells;     /* Door u_int order (row-major argwhere 'D') */
   int32_t door_closed_on_init, door_auto_close;
-  int32_t pomdp_r;
+  int32_t pomdp_r;               /* 0 = full observability: the window is the whole level (H x W), absolute cells,
+                                    rays of radius min(H, W) (observation_builder.py:51,154-158) */
   int32_t n_rays;
   const int32_t* ray_off;        /* [n_rays+1] prefix offsets into ray_pts (in points) */
   const int32_t* ray_pts;        /* [points][2] (dx, dy) from the ray origin, Bresenham order (ray_caster.py:141-199) */
   int32_t n_agents;
   int32_t agent_blocking[MFG_MAX_AGENTS];
+  int32_t n_positions[MFG_MAX_AGENTS];                      /* Agents.<name>.Positions (config_parser.py:181) */
+  int32_t positions[MFG_MAX_AGENTS][MFG_MAX_POSITIONS];     /* cells; SpawnAgents takes the first empty one (rules.py:187-196) */
   int32_t n_actions[MFG_MAX_AGENTS];
   mfg_action actions[MFG_MAX_AGENTS][MFG_MAX_ACTIONS];
   int32_t n_layers[MFG_MAX_AGENTS];
@@ -149,6 +160,12 @@ typedef struct mfg_spec {
   int32_t has_doors;
   int32_t n_rules;
   mfg_rule rules[MFG_MAX_RULES];
+  /* SpawnDestinationsPerAgent entries in YAML order: the agent, a coordinate list (q = 0) or a quantity q > 0 */
+  int32_t n_dest_entries;
+  int32_t dest_entry_agent[MFG_MAX_AGENTS];
+  int32_t dest_entry_q[MFG_MAX_AGENTS];
+  int32_t dest_entry_n[MFG_MAX_AGENTS];
+  int32_t dest_entry_cells[MFG_MAX_AGENTS][MFG_MAX_POSITIONS];
   int32_t individual_rewards;
   uint32_t env_seed;
 } mfg_spec;

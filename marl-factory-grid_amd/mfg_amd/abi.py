@@ -8,6 +8,7 @@ MAX_LAYERS = 32
 MAX_COMBINED = 72
 MAX_RULES = 32
 MAX_DOORS = 64
+MAX_POSITIONS = 16
 
 # action opcodes
 ACT_NOOP, ACT_MOVE, ACT_CHARGE, ACT_CLEAN, ACT_DEST, ACT_DOORUSE, ACT_ITEM, ACT_MACHINE = range(8)
@@ -27,7 +28,8 @@ LAYER_ZERO, LAYER_TAG, LAYER_COMBINED, LAYER_BATTERY, LAYER_GLOBALPOS = range(5)
  RULE_SPAWN_DIRT, RULE_SPAWN_DESTS, RULE_SPAWN_MACHINES, RULE_SPAWN_MAINTAINERS, RULE_SPAWN_GLOBALPOS,
  RULE_DOOR_AUTOCLOSE, RULE_RESPAWN_ITEMS, RULE_WATCH_COLLISIONS, RULE_BATTERY_DECHARGE, RULE_DONE_BATTERY,
  RULE_DONE_MAXSTEPS, RULE_RESPAWN_DIRT, RULE_SMEAR_DIRT, RULE_DONE_DIRT, RULE_DEST_REACH, RULE_DONE_DEST,
- RULE_MOVE_MAINTAINERS, RULE_DONE_MAINT_COLLISION) = range(1, 24)
+ RULE_MOVE_MAINTAINERS, RULE_DONE_MAINT_COLLISION, RULE_SPAWN_DEST_ON_AGENT, RULE_SPAWN_DEST_PER_AGENT,
+ RULE_RANDOM_INIT_STEPS) = range(1, 27)
 
 DEST_ANY, DEST_ALL, DEST_SIMULTANEOUS = range(3)
 
@@ -45,7 +47,7 @@ CRASH_NAMES = {0: 'none', 1: 'reference crash path (DestAction on a destination 
 
 class MfgAction(C.Structure):
     _fields_ = [('op', C.c_int32), ('arg', C.c_int32), ('valid_reward', C.c_double), ('fail_reward', C.c_double),
-                ('aux0', C.c_double), ('aux1', C.c_double)]
+                ('aux0', C.c_double), ('aux1', C.c_double), ('battery_cost', C.c_double)]
 
 
 class MfgLayer(C.Structure):
@@ -69,6 +71,8 @@ class MfgSpec(C.Structure):
         ('n_rays', C.c_int32), ('ray_off', C.POINTER(C.c_int32)), ('ray_pts', C.POINTER(C.c_int32)),
         ('n_agents', C.c_int32),
         ('agent_blocking', C.c_int32 * MAX_AGENTS),
+        ('n_positions', C.c_int32 * MAX_AGENTS),
+        ('positions', (C.c_int32 * MAX_POSITIONS) * MAX_AGENTS),
         ('n_actions', C.c_int32 * MAX_AGENTS),
         ('actions', (MfgAction * MAX_ACTIONS) * MAX_AGENTS),
         ('n_layers', C.c_int32 * MAX_AGENTS),
@@ -92,6 +96,11 @@ class MfgSpec(C.Structure):
         ('has_doors', C.c_int32),
         ('n_rules', C.c_int32),
         ('rules', MfgRule * MAX_RULES),
+        ('n_dest_entries', C.c_int32),
+        ('dest_entry_agent', C.c_int32 * MAX_AGENTS),
+        ('dest_entry_q', C.c_int32 * MAX_AGENTS),
+        ('dest_entry_n', C.c_int32 * MAX_AGENTS),
+        ('dest_entry_cells', (C.c_int32 * MAX_POSITIONS) * MAX_AGENTS),
         ('individual_rewards', C.c_int32),
         ('env_seed', C.c_uint32),
     ]

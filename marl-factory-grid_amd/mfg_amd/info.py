@@ -38,8 +38,12 @@ def rebuild_info(spec, actions, ev, reward):
         if op == abi.RULE_DOOR_AUTOCLOSE and g('door_autoclose'):
             info[f'Global_{rname}'] += 1
         elif op in (abi.RULE_BATTERY_DECHARGE, abi.RULE_DONE_BATTERY):
-            for n in names:
-                info[f'{n}_{rname}'] += rf[0]
+            for a, n in enumerate(names):
+                if ri_[2]:  # per_action_costs[agent.state.identifier]: the action's class, 'Noop' if paralyzed
+                    cls = spec.agent_actions[a][int(actions[a])]['cls'] if act[a] & 0x80 else 'Noop'
+                    info[f'{n}_{rname}'] += spec.battery_cost_dict[cls]
+                else:
+                    info[f'{n}_{rname}'] += rf[0]
         elif op == abi.RULE_RESPAWN_DIRT and g('dirt_spawn_value') >= 0:
             info['Global_DirtPiles_spawn'] += g('dirt_spawn_value')
         elif op in (abi.RULE_DEST_REACH, abi.RULE_DONE_DEST):

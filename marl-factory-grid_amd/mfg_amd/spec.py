@@ -70,8 +70,24 @@ _RULES = {
     'RespawnDirt': abi.RULE_RESPAWN_DIRT, 'EntitiesSmearDirtOnMove': abi.RULE_SMEAR_DIRT,
     'DoneOnAllDirtCleaned': abi.RULE_DONE_DIRT, 'DestinationReachReward': abi.RULE_DEST_REACH,
     'DoneAtDestinationReach': abi.RULE_DONE_DEST, 'MoveMaintainers': abi.RULE_MOVE_MAINTAINERS,
-    'DoneAtMaintainerCollision': abi.RULE_DONE_MAINT_COLLISION,
+    'DoneAtMaintainerCollision': abi.RULE_DONE_MAINT_COLLISION, 'DoRandomInitialSteps': abi.RULE_RANDOM_INIT_STEPS,
 }
+# Destinations `spawnrule` classes (modules/destinations/rules.py:95-162)
+_DEST_SPAWNRULES = {'SpawnDestinationOnAgent': abi.RULE_SPAWN_DEST_ON_AGENT,
+                    'SpawnDestinationsPerAgent': abi.RULE_SPAWN_DEST_PER_AGENT}
+
+
+def _literal_cells(values, H, W, what):
+    """'(x, y)' strings (ast.literal_eval, config_parser.py:181 / destinations/rules.py:111) -> cell indices."""
+    cells = []
+    for v in values:
+        xy = ast.literal_eval(v) if isinstance(v, str) else tuple(v)
+        if len(xy) != 2 or not (0 <= int(xy[0]) < H and 0 <= int(xy[1]) < W):
+            raise UnsupportedSpec(f'{what}: position {v!r} outside the {H}x{W} level')
+        cells.append(int(xy[0]) * W + int(xy[1]))
+    if len(cells) > abi.MAX_POSITIONS:
+        raise UnsupportedSpec(f'{what}: more than {abi.MAX_POSITIONS} positions')
+    return cells
 
 
 def ray_table(d: int, n_rays: int = 100, degs: int = 360):
@@ -140,7 +156,19 @@ class EnvSpec:
 
     @property
     def d(self):
+        """window diameter (pomdp_r > 0); with pomdp_r == 0 the window is the level, see obs_hw"""
         return 2 * self.pomdp_r + 1
+
+    @property
+    def obs_hw(self):
+        """(h, w) of one observation layer: (d, d), or the level shape with full observability
+        (observation_builder.py:51)"""
+        return (self.d, self.d) if self.pomdp_r else (self.H, self.W)
+
+    @property
+    def ray_radius(self):
+        """RayCaster radius = min(obs_shape) (observation_builder.py:244; Q13)"""
+        return min(self.obs_hw)
 
     @property
     def n_layers(self):
@@ -235,10 +263,12 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
     lvl = Path(custom_level_path) if custom_level_path else LEVELS_DIR / f'{level_name}.txt'
     H, W, level, floor, walls, doors = _parse_level(lvl)
     pomdp_r = int(gen['pomdp_r'])
-    if pomdp_r <= 0:
-        raise UnsupportedSpec('pomdp_r == 0 (full observability) is not implemented by the engine yet')
+    if pomdp_r < 0:
+        raise UnsupportedSpec('pomdp_r must be >= 0')
+    if pomdp_r == 0 and (min(H, W) > 30 or H * W > 4095):
+        raise UnsupportedSpec('full observability (pomdp_r 0) is limited to levels with min(H, W) <= 30, H*W < 4096')
     d = 2 * pomdp_r + 1
-    size = pomdp_r ** 2  # LevelParser.size (level_parser.py:440), non-positional collection cap (Q16)
+    size = pomdp_r ** 2 if pomdp_r else H * W  # LevelParser.size (level_parser.py:44), collection cap (Q16)
 
     # ---- entities (config_parser.py:80-126), YAML order ----
     ents = cfg.get('Entities') or {}
@@ -255,10 +285,9 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
 
     # ---- agents (config_parser.py:128-199) ----
     agents_conf = cfg['Agents']
-    agent_names, agent_actions, agent_obs, agent_blocking = [], [], [], []
+    agent_names, agent_actions, agent_obs, agent_blocking, agent_positions = [], [], [], [], []
     for name, ac in agents_conf.items():
-        if ac.get('Positions'):
-            raise UnsupportedSpec('configured agent Positions are not implemented by the engine yet')
+        positions = _literal_cells(ac.get('Positions') or [], H, W, f'Agents.{name}.Positions')
         acts = _parse_actions(ac['Actions'])
         obs = []
         if ac.get('Observations') is None:
@@ -277,11 +306,12 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
             if isinstance(clones, int):
                 clones = [f'{name}_the_{n}{_n_abbr(n)}' for n in range(clones)]
             names += list(clones)
-        for n in names:
+        for n in names:  # clones share the conf, Positions included (config_parser.py:189-194)
             agent_names.append(n)
             agent_actions.append(acts)
             agent_obs.append(obs)
             agent_blocking.append(blocking)
+            agent_positions.append(positions)
     A = len(agent_names)
     if A > abi.MAX_AGENTS:
         raise UnsupportedSpec(f'{A} agents > {abi.MAX_AGENTS}')
@@ -353,6 +383,8 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
     if 'Defaults' in rules_conf:
         raise UnsupportedSpec("Rules: Defaults loads 'WatchCollision' and exits upstream (Q23)")
     rules, rule_names = [], []
+    battery_cost_dict = None
+    dest_entries = []
     for rname, rkw in rules_conf.items():
         rkw = rkw or {}
         if rname not in _RULES:
@@ -372,8 +404,17 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
         elif op in (abi.RULE_BATTERY_DECHARGE, abi.RULE_DONE_BATTERY):
             cost = rkw.get('per_action_costs', 0.02)
             if isinstance(cost, dict):
-                raise UnsupportedSpec('per-action battery cost dicts are not implemented by the engine yet')
-            rf[0] = float(cost)
+                # energy_consumption = per_action_costs[agent.state.identifier] (batteries/rules.py:54-58): keyed
+                # by the ActionResult identifier = the action's class name; a paralyzed agent's state is 'Noop'
+                cost = {str(k): float(v) for k, v in cost.items()}
+                if battery_cost_dict is not None and battery_cost_dict != cost:
+                    raise UnsupportedSpec('two battery rules with different per_action_costs dicts')
+                battery_cost_dict = cost
+                ri[2] = 1
+                ri[3] = int('Noop' in cost)
+                rf[3] = cost.get('Noop', 0.0)
+            else:
+                rf[0] = float(cost)
             rf[1] = float(rkw.get('battery_discharge_reward', -1.0))
             ri[0] = int(bool(rkw.get('paralyze_agents_on_discharge', False)))
             if op == abi.RULE_DONE_BATTERY:
@@ -398,6 +439,10 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
             rf[1] = float(rkw.get('reward_at_done', 5.0))
             ri[0] = {'any': abi.DEST_ANY, 'all': abi.DEST_ALL, 'simultaneous': abi.DEST_SIMULTANEOUS}[
                 rkw.get('condition', 'any')]
+        elif op == abi.RULE_RANDOM_INIT_STEPS:
+            if 'random_steps' not in rkw:  # `def __init__(self, random_steps: 10)` has no default (rules.py:329)
+                raise UnsupportedSpec('DoRandomInitialSteps needs random_steps (TypeError upstream)')
+            ri[0] = int(rkw['random_steps'])
         rules.append((op, ri, rf))
         rule_names.append(rname)
     # spawn rules in Entities order (Walls, Agents have none)
@@ -406,8 +451,30 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
         op = _GROUPS[g][1]
         if op is None:
             continue
-        if kw.get('spawnrule'):
-            raise UnsupportedSpec('custom spawnrule is not implemented by the engine yet')
+        if kw.get('spawnrule'):  # Collection.spawn_rule (collection.py:66-77): the given rule replaces SpawnEntity
+            if g != 'Destinations':
+                raise UnsupportedSpec(f'{g}: spawnrule is only implemented for Destinations')
+            for sr_name, sr_kw in kw['spawnrule'].items():
+                if sr_name not in _DEST_SPAWNRULES:
+                    raise UnsupportedSpec(f'spawnrule {sr_name!r} is not implemented by the engine')
+                sr_kw = sr_kw or {}
+                if sr_name == 'SpawnDestinationsPerAgent':
+                    if set(sr_kw) != {'coords_or_quantity'} or not isinstance(sr_kw['coords_or_quantity'], dict):
+                        raise UnsupportedSpec('SpawnDestinationsPerAgent takes coords_or_quantity: {agent: [...]}')
+                    for an, val in sr_kw['coords_or_quantity'].items():
+                        # agent = get_first(state[AGENT], lambda x: agent_name in x.name) (rules.py:114)
+                        hit = [i for i, n in enumerate(agent_names) if str(an) in f'Agent[{n}]']
+                        if not hit:
+                            raise UnsupportedSpec(f'SpawnDestinationsPerAgent: no agent matches {an!r} (assert upstream)')
+                        if isinstance(val, int):
+                            dest_entries.append((hit[0], val, []))
+                        else:
+                            dest_entries.append((hit[0], 0, _literal_cells(val, H, W, f'destinations of {an}')))
+                elif sr_kw:
+                    raise UnsupportedSpec(f'{sr_name} takes no kwargs')
+                rules.append((_DEST_SPAWNRULES[sr_name], [0] * 6, [0.0] * 6))
+                rule_names.append(sr_name)
+            continue
         ri, rf = [0] * 6, [0.0] * 6
         q = kw.get('coords_or_quantity')
         if op in (abi.RULE_SPAWN_PODS, abi.RULE_SPAWN_DROPOFFS, abi.RULE_SPAWN_ITEMS, abi.RULE_SPAWN_DESTS,
@@ -428,7 +495,9 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
         if g in group_names and cap_needed > size + 1:
             raise UnsupportedSpec(f'{g}: {cap_needed} agents exceed LevelParser.size+1={size + 1} (Q16)')
 
-    rays = ray_table(d)
+    if len(dest_entries) > abi.MAX_AGENTS:
+        raise UnsupportedSpec('too many SpawnDestinationsPerAgent entries')
+    rays = ray_table(d if pomdp_r else min(H, W))  # RayCaster(agent, min(obs_shape)) (Q13)
     ray_off = np.zeros(len(rays) + 1, np.int32)
     ray_off[1:] = np.cumsum([len(r) for r in rays])
     ray_pts = np.asarray([p for r in rays for p in r], np.int32).reshape(-1)
@@ -447,6 +516,9 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
     es.rules = rules
     es.ekw = ekw
     es.agent_blocking = agent_blocking
+    es.agent_positions = agent_positions
+    es.battery_cost_dict = battery_cost_dict
+    es.dest_entries = dest_entries
     es.c = _to_c(es)
     return es
 
@@ -481,6 +553,9 @@ def _to_c(es: EnvSpec) -> abi.MfgSpec:
     s.n_agents = es.n_agents
     for a in range(es.n_agents):
         s.agent_blocking[a] = int(es.agent_blocking[a])
+        s.n_positions[a] = len(es.agent_positions[a])
+        for j, cell in enumerate(es.agent_positions[a]):
+            s.positions[a][j] = cell
         acts = es.agent_actions[a]
         if len(acts) > abi.MAX_ACTIONS:
             raise UnsupportedSpec('too many actions')
@@ -492,6 +567,8 @@ def _to_c(es: EnvSpec) -> abi.MfgSpec:
             s.actions[a][j].fail_reward = ac['fail']
             s.actions[a][j].aux0 = ac['aux0']
             s.actions[a][j].aux1 = ac['aux1']
+            bc = es.battery_cost_dict
+            s.actions[a][j].battery_cost = (bc.get(ac['cls'], float('nan')) if bc is not None else 0.0)
         s.n_layers[a] = len(es.layer_prog[a])
         for j, (kind, tag) in enumerate(es.layer_prog[a]):
             s.layers[a][j].kind = kind
@@ -531,6 +608,13 @@ def _to_c(es: EnvSpec) -> abi.MfgSpec:
         for q in range(6):
             s.rules[j].i[q] = ri[q]
             s.rules[j].f[q] = rf[q]
+    s.n_dest_entries = len(es.dest_entries)
+    for j, (agent, q, cells) in enumerate(es.dest_entries):
+        s.dest_entry_agent[j] = agent
+        s.dest_entry_q[j] = q
+        s.dest_entry_n[j] = len(cells)
+        for k, cell in enumerate(cells):
+            s.dest_entry_cells[j][k] = cell
     s.individual_rewards = int(es.individual_rewards)
     s.env_seed = es.env_seed & 0xFFFFFFFF
     return s

@@ -83,7 +83,7 @@ class OracleEnv:
         self.h = self.L.oracle_create(C.byref(spec.c), _p(key), len(key))
         self.A = spec.n_agents
         self.d = spec.d
-        self._obs = np.zeros((self.A, abi.MAX_LAYERS, self.d, self.d), np.float64)
+        self._obs = np.zeros((self.A, abi.MAX_LAYERS) + tuple(spec.obs_hw), np.float64)
         self._rew = np.zeros(self.A, np.float64)
         self._done = np.zeros(1, np.uint8)
         self.ev = abi.MfgEvents()

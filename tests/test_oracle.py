@@ -11,7 +11,10 @@ import golden_compare as G
 UNITS = np.load(G.GOLDEN / 'units.npz')
 FIXTURES = [('large8', 'large8.yaml'), ('rooms4', 'rooms4.yaml'), ('simple1', 'simple1.yaml'),
             ('alltest16', 'alltest16.yaml'), ('default_large', 'default_large.yaml'),
-            ('maint_rooms', 'maint_rooms.yaml'), ('grid128_64', 'grid128_64.yaml')]
+            ('maint_rooms', 'maint_rooms.yaml'), ('grid128_64', 'grid128_64.yaml'),
+            ('eight_puzzle', 'eight_puzzle.yaml'), ('narrow_corridor', 'narrow_corridor.yaml'),
+            ('_obs_test', '_obs_test.yaml'), ('puzzle_dest_crash', 'puzzle_dest_crash.yaml'),
+            ('corridor_quantity', 'corridor_quantity.yaml')]
 
 
 def test_mt19937_matches_cpython():
