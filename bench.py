@@ -271,7 +271,7 @@ def main():
             t = torch.tensor([el2], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el2 = float(t.item())
-        alt_obs_bytes = sum(spec.n_layers) * spec.d * spec.d * (8 if alt_dtype == 'f64' else 4)
+        alt_obs_bytes = sum(spec.n_layers) * spec.obs_hw[0] * spec.obs_hw[1] * (8 if alt_dtype == 'f64' else 4)
         alt_step_bytes = core_bytes(spec) + alt_obs_bytes
         alt_value = B * world * alt_steps / el2
         alt = {"obs": alt_dtype, "value": round(alt_value, 1), "unit": "env-steps/s", "steps": alt_steps,
@@ -285,7 +285,7 @@ def main():
         mean_call = sum(t for t, _ in full) / len(full)
         k_call = full[0][1]
         obs_el = 8 if args.obs_dtype == 'f64' else 4
-        obs_bytes = sum(spec.n_layers[a] for a in range(A)) * spec.d * spec.d * obs_el
+        obs_bytes = sum(spec.n_layers[a] for a in range(A)) * spec.obs_hw[0] * spec.obs_hw[1] * obs_el
         busy = sum(ms for ms, n in prof.values())
         kernels = {}
         for name, (ms, n) in prof.items():

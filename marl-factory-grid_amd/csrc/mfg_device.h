@@ -56,6 +56,9 @@ static_assert(H__END <= MFG_HDR_N, "header overflow");
 #define EW_PRESENT 0x20000   // present in the global pos_dict (identifier-dedup may keep it out, Q14)
 #define EW_REACHED 0x40000   // destination reached
 #define EW_NOPOS 0xFFFF
+// destination bound to an agent (Object.bind_to, entity/object.py:140-148): bits 20..26 = agent index + 1
+#define EW_BOUND_SHIFT 20
+#define EW_BOUND(w) ((((w) >> EW_BOUND_SHIFT) & 0x7F) - 1)
 // door word: bit0 open, bits 8..15 time_to_close, bit16 present in the global pos_dict
 #define DW_OPEN 1
 #define DW_TTC(w) (((w) >> 8) & 0xFF)
@@ -84,7 +87,10 @@ struct MfgLayerRec {
 
 struct MfgDevSpec {
   mfg_spec s;  // table pointers inside are HOST pointers: never dereferenced on the device
-  int32_t HW, nf, nw, nd, A, r, d, dd, nrays, maxpts, lmax;
+  // window: r = pomdp_r; oh x ow = (2r+1)^2 around the agent, or the whole level (r = 0, full observability,
+  // observation_builder.py:51,154-158), dd = oh * ow cells. fr = ray radius = min(oh, ow) (Q13): the first-visit
+  // table spans (2 fr + 1)^2 cells around the ray origin.
+  int32_t HW, nf, nw, nd, A, r, oh, ow, dd, fr, nrays, maxpts, lmax;
   int32_t imax, pmax, dropmax, destmax;
   int32_t obs_agent_stride;  // lmax*dd
   const uint8_t* level;      // [HW] 0 floor 1 wall 2 door

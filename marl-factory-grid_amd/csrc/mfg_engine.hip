@@ -845,12 +845,12 @@ __device__ int spawn_positions(const Env& e, int n, int ignore_blocking, int* ou
 // ------------------------------------------------------------------------------------------------
 // append one int-id entity to a group table; it enters the global pos_dict only if no entity with an
 // equal identifier is already there (Objects.notify_add_entity, objects.py:203-214)
-__device__ void spawn_into(const Env& e, int* tbl, int hn, int base, int cell) {
+__device__ void spawn_into(const Env& e, int* tbl, int hn, int base, int cell, int extra = 0) {
   int n = e.H(hn);
   int slot;
   int id = base + n;
   bool present = find_present_id(e, cell, id, &slot) == K_NONE;
-  if (e.lane == 0) tbl[n] = cell | EW_ALIVE | (present ? EW_PRESENT : 0);
+  if (e.lane == 0) tbl[n] = cell | EW_ALIVE | (present ? EW_PRESENT : 0) | extra;
   e.setH(hn, n + 1);
   wave_sync();
 }
@@ -940,6 +940,7 @@ struct StepOut {
   double g_rew;       // uniform: 'global' reward sum
   int my_act_ev;      // lane a: act event bits
   int my_watch_ev;    // lane a: watch event bits
+  int my_slot;        // lane a: action slot agent a executed this step, -1 if it did not act (paralyzed)
   uint64_t door_coll;
   uint32_t maint_coll;  // maintainers (collection slots) that received a WatchCollisions result
   int respawn_items_value, dirt_spawn_value, dirt_spawn_valid, door_autoclose, done_mask, dest_reached, crashed;
@@ -1430,13 +1431,19 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
       wave_sync();
     }
   } else if (op == MFG_RULE_BATTERY_DECHARGE || op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:50-64
+    bool missing = false;
     if (e.lane < S->A) {
+      double cost = ru.f[0];
+      if (ru.i[2])  // per_action_costs[agent.state.identifier]: the executed action's class, 'Noop' if paralyzed
+        cost = o.my_slot >= 0 ? S->s.actions[e.lane][o.my_slot].battery_cost : (ru.i[3] ? ru.f[3] : __builtin_nan(""));
+      missing = cost != cost;
       double b = e.bat()[e.lane];
-      if (b != 0.0) {
-        double nv = ru.f[0] + b;
+      if (b != 0.0 && !missing) {
+        double nv = cost + b;
         e.bat()[e.lane] = nv > 0.0 ? nv : 0.0;
       }
     }
+    if (ballot(missing)) o.crashed = MFG_CRASH_RULE;  // KeyError upstream
     wave_sync();
   } else if (op == MFG_RULE_RESPAWN_DIRT) {  // clean_up/rules.py:49-59
     int c = uni(e.rctr()[ri]);
@@ -1470,6 +1477,8 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
       const int cell = EW_POS(w);
       const u64 am = agents_at(e, cell);
       if (!am) continue;
+      const int bnd = EW_BOUND(w);  // a bound destination is reached only by its agent (rules.py:40-46)
+      if (bnd >= 0 && !((am >> bnd) & 1)) continue;
       // the Agents-group cell list is in arrival order; the loop variable ends on the last arrival
       int arr = e.lane < S->A && ((am >> e.lane) & 1) ? e.agarr()[e.lane] : -1;
       int best = arr;
@@ -1623,7 +1632,8 @@ __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
 // ------------------------------------------------------------------------------------------------
 __device__ void env_reset(const Env& e, int* scratch) {
   SpecP S = e.S;
-  const int A = S->A;
+  const int A = S->A, W = S->s.W;
+  int reset_crash = 0;  // a reference exception inside reset(): reported by the next step (crashed + done)
   pay_debt(e);
   // OBSBuilder keeps the episode-1 agent / battery objects for its ray origins and bound layers
   if (e.H(H_OBS_INIT) && !e.H(H_FROZEN)) {
@@ -1660,15 +1670,29 @@ __device__ void env_reset(const Env& e, int* scratch) {
     const int j = mt_randbelow_seq<uint16_t>(e, m - 1, m - 1, nullptr);  // first Fisher-Yates step picks the last slot
     if (m - 2 >= 1) mt_randbelow_seq<uint16_t>(e, m - 2, 1, nullptr);     // remaining draws of shuffle(empty_positions)
     int k = 0, cell = -1;
-    for (int b = 0; b < nf && cell < 0; b += MFG_WAVE) {
-      const int i = b + e.lane;
-      const bool em = i < nf && lane_cell_empty(e, perm[i < nf ? i : 0]);
-      const u64 mm = ballot(em);
-      const int rank = k + mbcnt(mm);
-      const u64 hitm = ballot(em && rank == j);
-      if (hitm) cell = rl(i < nf ? (int)perm[i] : 0, ffs64(hitm));
-      k += popc(mm);
+    const int npos = S->s.n_positions[a];
+    if (npos > 0) {
+      // configured Positions: get_first(x for x in positions if x in empty_positions) (rules.py:191-193, Q24),
+      // then `assert state.check_pos_validity(position)`: one more floor shuffle (Q3); none -> ValueError
+      for (int q = 0; q < npos && cell < 0; q++) {
+        const int c = S->s.positions[a][q];
+        if (S->level[c] != 1 && uni((int)lane_cell_empty(e, c))) cell = c;
+      }
+      if (cell >= 0) floor_shuffle(e);
+      else reset_crash = MFG_CRASH_RULE;
+    } else {
+      for (int b = 0; b < nf && cell < 0; b += MFG_WAVE) {
+        const int i = b + e.lane;
+        const bool em = i < nf && lane_cell_empty(e, perm[i < nf ? i : 0]);
+        const u64 mm = ballot(em);
+        const int rank = k + mbcnt(mm);
+        const u64 hitm = ballot(em && rank == j);
+        if (hitm) cell = rl(i < nf ? (int)perm[i] : 0, ffs64(hitm));
+        k += popc(mm);
+      }
+      if (cell < 0) reset_crash = MFG_CRASH_RULE;  // empty_positions.pop() on an empty list
     }
+    if (cell < 0) cell = S->floor_init[0];
     wave_sync();
     if (e.lane == 0) { e.agpos()[a] = cell; e.agarr()[a] = a; }
     e.setH(H_CNT_AGENT, e.H(H_CNT_AGENT) + 1);
@@ -1706,6 +1730,51 @@ __device__ void env_reset(const Env& e, int* scratch) {
       dirt_trigger_spawn(e, S->s.dirt_quantity, 0.0, &v, scratch);
     } else if (op == MFG_RULE_SPAWN_GLOBALPOS) {
       e.setH(H_CNT_GP, e.H(H_CNT_GP) + A);
+    } else if (op == MFG_RULE_SPAWN_DEST_ON_AGENT) {  // destinations/rules.py:155-162: bound, on the agent's cell
+      const int base = e.H(H_CNT_DEST);
+      e.setH(H_DEST_BASE, base);
+      for (int a = 0; a < A; a++) spawn_into(e, e.dests(), H_N_DESTS, base, uni(e.agpos()[a]), (a + 1) << EW_BOUND_SHIFT);
+      e.setH(H_CNT_DEST, base + A);
+      wave_sync();
+    } else if (op == MFG_RULE_SPAWN_DEST_PER_AGENT) {  // destinations/rules.py:116-133
+      const int base = e.H(H_CNT_DEST);
+      e.setH(H_DEST_BASE, base);
+      int made = 0;
+      // candidate list after the 128 B of shuffle sink words at the start of the scratch
+      uint16_t* l16 = (uint16_t*)((uint8_t*)scratch + 128);
+      int* l32 = (int*)((uint8_t*)scratch + 128);
+      for (int j = 0; j < S->s.n_dest_entries && !reset_crash; j++) {
+        const int a = S->s.dest_entry_agent[j], apos = uni(e.agpos()[a]);
+        const bool quant = S->s.dest_entry_q[j] > 0;
+        int n;
+        if (quant) {  // position_list = state.entities.floorlist (a shuffled copy), shuffled once more
+          floor_shuffle(e);
+          for (int i = e.lane; i < S->nf; i += MFG_WAVE) l16[i] = e.perm()[i];
+          wave_sync();
+          floor_shuffle_t(e, l16);
+          n = S->nf;
+        } else {      // coordinate list: shuffle(position_list) (random.py:380-395)
+          n = S->s.dest_entry_n[j];
+          if (e.lane < n) l32[e.lane] = S->s.dest_entry_cells[j][e.lane];
+          wave_sync();
+          for (int i = n - 1; i > 0; i--) {
+            const int r2 = mt_randbelow1(e, i + 1);
+            if (e.lane == 0) { const int t = l32[i]; l32[i] = l32[r2]; l32[r2] = t; }
+            wave_sync();
+          }
+        }
+        int cell = -1;  // pop() until a cell that is not the agent's and holds no destination; one per entry
+        while (n > 0 && cell < 0) {
+          const int c = quant ? (int)l16[n - 1] : uni(l32[n - 1]);
+          n--;
+          if (c != apos && !grp_at(e.dests(), e.H(H_N_DESTS), c, EW_ALIVE, e.lane)) cell = c;
+        }
+        if (cell < 0) { reset_crash = MFG_CRASH_RULE; break; }  // exit(-9999) upstream
+        spawn_into(e, e.dests(), H_N_DESTS, base, cell, (a + 1) << EW_BOUND_SHIFT);
+        made++;
+      }
+      e.setH(H_CNT_DEST, base + made);
+      wave_sync();
     } else if (op == MFG_RULE_SPAWN_MACHINES || op == MFG_RULE_SPAWN_MAINTAINERS) {
       const bool mach = op == MFG_RULE_SPAWN_MACHINES;
       const int q = ru.i[0];
@@ -1719,6 +1788,47 @@ __device__ void env_reset(const Env& e, int* scratch) {
     }
     wave_sync();
   }
+  // rules' on_reset_post_spawn in order (states.py:52-56): DoRandomInitialSteps (rules.py:341-355)
+  for (int r = 0; r < S->s.n_rules && !reset_crash; r++) {
+    const CS mfg_rule& ru = S->s.rules[r];
+    if (ru.op != MFG_RULE_RANDOM_INIT_STEPS) continue;
+    for (int k = 0; k < ru.i[0] && !reset_crash; k++) {
+      if (free_positions(e, 1, scratch) < 1) { reset_crash = MFG_CRASH_RULE; break; }  // random_free_position
+      const int fp = uni(scratch[0]);
+      const int fx = fp / W, fy = fp % W;
+      // neighboring_4_positions: POS_MASK_4 offsets (helpers.py:34, not N/E/S/W: Q23) that are floor cells
+      int* nb = scratch + 32;
+      int n = 0;
+      for (int q = 0; q < 6; q++) {
+        const int dx = q == 1 || q == 3 ? -1 : (q == 2 || q == 5 ? 1 : 0), dy = q == 0 ? -1 : (q >= 3 ? 1 : 0);
+        const int x = fx + dx, y = fy + dy;
+        if (x >= 0 && y >= 0 && x < S->s.H && y < W && S->level[x * W + y] != 1) {
+          if (e.lane == 0) nb[n] = x * W + y;
+          n++;
+        }
+      }
+      wave_sync();
+      for (int i = n - 1; i > 0; i--) {  // random.shuffle(neighbor_positions)
+        const int r2 = mt_randbelow1(e, i + 1);
+        if (e.lane == 0) { const int t = nb[i]; nb[i] = nb[r2]; nb[r2] = t; }
+        wave_sync();
+      }
+      const int p = n ? uni(nb[n - 1]) : -1;
+      const u64 am = p >= 0 ? agents_at(e, p) : 0ull;
+      if (!am) { reset_crash = MFG_CRASH_RULE; break; }  // pop() on an empty list / assert isinstance(.., Agent)
+      // get_first(by_pos(p)): the Agents group lists a cell's agents in arrival order
+      int arr = e.lane < A && ((am >> e.lane) & 1) ? e.agarr()[e.lane] : 0x7FFFFFFF;
+      for (int o2 = 32; o2 > 0; o2 >>= 1) arr = min(arr, __shfl_xor(arr, o2));
+      const int a = ffs64(ballot(e.lane < A && ((am >> e.lane) & 1) && e.agarr()[e.lane < A ? e.lane : 0] == arr));
+      // chosen_agent.move(free_pos) (entity.py:175-199): check_move_validity once (states.py:240-270, Q3)
+      const bool blocked = blocked_at(e, fp);
+      if (!blocked) floor_shuffle(e);
+      const bool not_blocked = !blocked && S->level[fp] != 1;
+      const bool blocking_others = S->s.agent_blocking[a] && (colliders_at(e, fp) > 0 || blocked);
+      if (p != fp && not_blocked && !blocking_others) set_agent_pos(e, a, fp);
+    }
+  }
+  if (reset_crash) e.setH(H_CRASHED, reset_crash);
   e.setH(H_EPISODE, e.H(H_EPISODE) + 1);
   wave_sync();
 }
@@ -1918,7 +2028,7 @@ struct Sup {  // per-agent suppression sets from the identifier dedupe
   u64 items, pods, drops, dests, doors, machines, maints;
   uint8_t* wsup;   // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
   __attribute__((address_space(3))) uint32_t* dsup;  // dirt slots: LDS bitmap [dirt_cap / 32]
-  int ax, ay, r, d, W;
+  int wx0, wy0, oh, ow, W;  // window origin cell and shape
   __device__ __forceinline__ bool dirt_sup(int i) const {
     return ((dsup[i >> 5] >> (i & 31)) & 1u) != 0;
   }
@@ -1938,8 +2048,8 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
     case K_MACHINE: s.machines |= bit; break;
     case K_MAINT: s.maints |= bit; break;
     default: {
-      const int px = (xy >> 16) - s.ax + s.r, py = (xy & 0xFFFF) - s.ay + s.r;
-      if (px >= 0 && py >= 0 && px < s.d && py < s.d && lane == 0) s.wsup[px * s.d + py] = 1;
+      const int px = (xy >> 16) - s.wx0, py = (xy & 0xFFFF) - s.wy0;
+      if (px >= 0 && py >= 0 && px < s.oh && py < s.ow && lane == 0) s.wsup[px * s.ow + py] = 1;
       break;
     }
   }
@@ -1948,8 +2058,11 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
 template <int MAXPTS, typename OT, bool MM>
 __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   SpecP S = e.S;
-  const int A = S->A, H = S->s.H, W = S->s.W, r = S->r, d = S->d, dd = S->dd;
-  const float invd = 1.0f / (float)d;
+  // window: oh x ow cells from (wx0, wy0) = agent - r, or the whole level at (0, 0) when pomdp_r == 0
+  // (observation_builder.py:152-158); rays and the first-visit table have radius fr (Q13)
+  const int A = S->A, H = S->s.H, W = S->s.W, oh = S->oh, ow = S->ow, dd = S->dd, fr = S->fr;
+  const bool full = S->r == 0;
+  const float invw = 1.0f / (float)ow;
   const int lane = e.lane;
   const bool frozen = e.H(H_FROZEN) != 0;
   build_cmap<MM>(e);
@@ -1968,7 +2081,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
   // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
   // ray * 32 + point; it gives both the window visibility and the dedupe order (Q14)
   uint32_t* fv = (uint32_t*)(e.scratch + 3 * S->pairs_lds);
-  const int fw = 2 * d + 1, fn = fw * fw;
+  const int fw = 2 * fr + 1;
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
   // dirt suppression bitmap for groups wider than a wave: after the per-lane sink words of the ray walk
@@ -1989,15 +2102,16 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
     const int apos = rl(agp, a);
     const int ax = rl(agx, a), ay = rl(agy, a);
     const int ox = rl(orgx, a), oy = rl(orgy, a);
+    const int wx0 = full ? 0 : ax - S->r, wy0 = full ? 0 : ay - S->r;
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
     for (int i = lane; i < 2 * dd; i += MFG_WAVE) amw[i] = 0u;
     wave_sync();
     if (lane < A) {  // scatter the agents into the window's agent masks
-      const int wx = agx - ax + r, wy = agy - ay + r;
-      if ((unsigned)wx < (unsigned)d && (unsigned)wy < (unsigned)d)
-        atomicOr((uint32_t*)&amw[2 * (wx * d + wy) + (lane >> 5)], 1u << (lane & 31));
+      const int wx = agx - wx0, wy = agy - wy0;
+      if ((unsigned)wx < (unsigned)oh && (unsigned)wy < (unsigned)ow)
+        atomicOr((uint32_t*)&amw[2 * (wx * ow + wy) + (lane >> 5)], 1u << (lane & 31));
     }
     // ---- ray walk (lane = ray, 64 rays per pass): blocking bits first, then the walk on bitmasks ----
 #ifdef MFG_ABLATE_OB_NORAY
@@ -2034,15 +2148,15 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
       // ray 0's rank 0, stored once below instead of a 64-lane same-address atomic
 #pragma unroll
       for (int p = 1; p < MAXPTS; p++)
-        atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + d) * fw + ray.dy(p) + d] : sink,
+        atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + fr) * fw + ray.dy(p) + fr] : sink,
                   (uint32_t)(ray_id * 32 + p));
     }
-    if (lane == 0) fv[d * fw + d] = 0u;
+    if (lane == 0) fv[fr * fw + fr] = 0u;
     wave_sync();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     Sup sup;
     sup.items = sup.pods = sup.drops = sup.dests = sup.doors = sup.machines = sup.maints = 0;
-    sup.ax = ax; sup.ay = ay; sup.r = r; sup.d = d; sup.W = W;
+    sup.wx0 = wx0; sup.wy0 = wy0; sup.oh = oh; sup.ow = ow; sup.W = W;
     sup.wsup = wsup;
     sup.dsup = dsup;
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
@@ -2050,8 +2164,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
       // the first pass's pair cells stay in registers across agents (the usual single pass)
       const int pA = q0 == 0 ? pA0 : (q < npairs ? pairs.get(q, 0) : 0);
       const int pB = q0 == 0 ? pB0 : (q < npairs ? pairs.get(q, 1) : 0);
-      const int xA = (pA >> 16) - ox + d, yA = (pA & 0xFFFF) - oy + d;
-      const int xB = (pB >> 16) - ox + d, yB = (pB & 0xFFFF) - oy + d;
+      const int xA = (pA >> 16) - ox + fr, yA = (pA & 0xFFFF) - oy + fr;
+      const int xB = (pB >> 16) - ox + fr, yB = (pB & 0xFFFF) - oy + fr;
       const bool nearq = (q < npairs) & ((unsigned)xA < (unsigned)fw) & ((unsigned)yA < (unsigned)fw) &
                          ((unsigned)xB < (unsigned)fw) & ((unsigned)yB < (unsigned)fw);
       const uint32_t rA0 = fv[nearq ? xA * fw + yA : 0], rB0 = fv[nearq ? xB * fw + yB : 0];
@@ -2079,9 +2193,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
       // wi / d and wi % d through a float reciprocal (exact: wi + 0.5 is >= 0.5 / d away from a multiple
       // of d, far above the rounding error for wi < 2^12); the tests below are branch-free, every LDS
       // read has a valid clamped address and its result is masked
-      const int wq = (int)(((float)wi + 0.5f) * invd), wr = wi - wq * d;
-      const int x = ax - r + wq, y = ay - r + wr;
-      const int lx = x - ox + d, ly = y - oy + d;
+      const int wq = (int)(((float)wi + 0.5f) * invw), wr = wi - wq * ow;
+      const int x = wx0 + wq, y = wy0 + wr;
+      const int lx = x - ox + fr, ly = y - oy + fr;
       const bool inb = inwin & ((unsigned)x < (unsigned)H) & ((unsigned)y < (unsigned)W) &
                        ((unsigned)lx < (unsigned)fw) & ((unsigned)ly < (unsigned)fw);
       const bool v = inb & (fv[inb ? lx * fw + ly : 0] != 0xFFFFFFFFu);
@@ -2192,15 +2306,17 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   const int A = S->A;
   o.my_rew = 0.0; o.g_rew = 0.0; o.my_act_ev = 0; o.my_watch_ev = 0; o.door_coll = 0; o.maint_coll = 0;
   o.respawn_items_value = -1; o.dirt_spawn_value = -1; o.dirt_spawn_valid = 0; o.door_autoclose = 0;
-  o.done_mask = 0; o.dest_reached = 0; o.crashed = 0; o.done = 0;
+  o.done_mask = 0; o.dest_reached = 0; o.crashed = 0; o.done = 0; o.my_slot = -1;
   e.setH(H_STEP, e.H(H_STEP) + 1);
   e.setH(H_TOTAL_STEPS, e.H(H_TOTAL_STEPS) + 1);
+  o.crashed = e.H(H_CRASHED);  // a crash the reset hit (or a crashed env stepped without a reset): done, no step
   wave_sync();
   for (int a = 0; a < A && !o.crashed; a++) {
     if (uni(e.agpar()[a])) continue;  // paralyzed agents skip their action
     const int slot = rl(my_act, a);
     if (slot < 0 || slot >= S->s.n_actions[a]) { o.crashed = MFG_CRASH_ACTION; break; }  // IndexError upstream
     do_action(e, o, a, slot);
+    if (e.lane == a) o.my_slot = slot;
   }
   const int nr = S->s.n_rules;
   if (!o.crashed)
@@ -2719,7 +2835,23 @@ static int validate_spec(const mfg_spec* s) {
   if (s->n_doors < 0 || s->n_doors > MFG_MAX_DOORS) return fail("too many doors");
   if (s->n_floor < 1 || s->n_floor > s->H * s->W || !s->floor_cells) return fail("n_floor out of range");
   if (s->n_walls < 0 || s->n_walls > s->H * s->W) return fail("n_walls out of range");
-  if (s->pomdp_r < 1 || s->pomdp_r > 8) return fail("engine supports pomdp_r in [1,8]");
+  if (s->pomdp_r < 0 || s->pomdp_r > 8) return fail("engine supports pomdp_r in [0,8]");
+  if (s->pomdp_r == 0 && (std::min(s->H, s->W) > 30 || s->H * s->W > 4095))
+    return fail("full observability (pomdp_r 0) needs min(H, W) <= 30 and H*W < 4096");
+  for (int a = 0; a < s->n_agents; a++) {
+    if (s->n_positions[a] < 0 || s->n_positions[a] > MFG_MAX_POSITIONS) return fail("n_positions out of range");
+    for (int k = 0; k < s->n_positions[a]; k++)
+      if (s->positions[a][k] < 0 || s->positions[a][k] >= s->H * s->W) return fail("agent position out of range");
+  }
+  if (s->n_dest_entries < 0 || s->n_dest_entries > MFG_MAX_AGENTS) return fail("n_dest_entries out of range");
+  for (int j = 0; j < s->n_dest_entries; j++) {
+    if (s->dest_entry_agent[j] < 0 || s->dest_entry_agent[j] >= s->n_agents) return fail("dest entry agent out of range");
+    if (s->dest_entry_q[j] < 0 || s->dest_entry_n[j] < 0 || s->dest_entry_n[j] > MFG_MAX_POSITIONS)
+      return fail("dest entry count out of range");
+    if (!s->dest_entry_q[j] && !s->dest_entry_n[j]) return fail("dest entry without positions");
+    for (int k = 0; k < s->dest_entry_n[j]; k++)
+      if (s->dest_entry_cells[j][k] < 0 || s->dest_entry_cells[j][k] >= s->H * s->W) return fail("dest cell out of range");
+  }
   if (s->n_rays < 1 || !s->ray_off || !s->ray_pts) return fail("empty ray table");
   if (s->n_rules < 0 || s->n_rules > MFG_MAX_RULES) return fail("n_rules out of range");
   for (int a = 0; a < s->n_agents; a++) {
@@ -2745,7 +2877,7 @@ static int validate_spec(const mfg_spec* s) {
     }
   }
   for (int r = 0; r < s->n_rules; r++)
-    if (s->rules[r].op < MFG_RULE_SPAWN_BATTERIES || s->rules[r].op > MFG_RULE_DONE_MAINT_COLLISION)
+    if (s->rules[r].op < MFG_RULE_SPAWN_BATTERIES || s->rules[r].op > MFG_RULE_RANDOM_INIT_STEPS)
       return fail("unknown rule opcode");
   for (int f = 0; f < s->n_floor; f++)
     if (s->floor_cells[f] < 0 || s->floor_cells[f] >= s->H * s->W) return fail("floor cell out of range");
@@ -2774,7 +2906,13 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   h.s = *s;
   const int HW = s->H * s->W;
   h.HW = HW; h.nf = s->n_floor; h.nw = s->n_walls; h.nd = s->n_doors; h.A = s->n_agents;
-  h.r = s->pomdp_r; h.d = 2 * s->pomdp_r + 1; h.dd = h.d * h.d; h.nrays = s->n_rays;
+  // window (observation_builder.py:51): (2r+1)^2, or the level with full observability; ray radius min(window)
+  h.r = s->pomdp_r;
+  h.oh = s->pomdp_r ? 2 * s->pomdp_r + 1 : s->H;
+  h.ow = s->pomdp_r ? 2 * s->pomdp_r + 1 : s->W;
+  h.dd = h.oh * h.ow;
+  h.fr = std::min(h.oh, h.ow);
+  h.nrays = s->n_rays;
   for (int a = 0; a < s->n_agents; a++) {  // combined layers that are plain member counts (MfgDevSpec)
     uint32_t tm = 0;
     uint64_t am = 0;
@@ -2796,7 +2934,13 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     h.comb_agents[a] = am;
   }
   if (h.nrays > 4 * MFG_WAVE) { delete e; return fail("more than 256 rays"); }
-  h.maxpts = 2 * s->pomdp_r + 2;
+  {  // points per ray (<= fr + 1), rounded up to a compiled k_obs instantiation (DISPATCH_MP)
+    int mp = 1;
+    for (int r = 0; r < h.nrays; r++) mp = std::max(mp, s->ray_off[r + 1] - s->ray_off[r]);
+    if (mp > 32) { delete e; return fail("rays longer than 32 points"); }
+    static const int SIZES[] = {4, 6, 8, 10, 12, 14, 16, 18, 24, 32};
+    for (int k : SIZES) if (k >= mp) { h.maxpts = k; break; }
+  }
   int lmax = 1;
   for (int a = 0; a < s->n_agents; a++) lmax = s->n_layers[a] > lmax ? s->n_layers[a] : lmax;
   h.lmax = lmax;
@@ -2808,6 +2952,8 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     if (ru.op == MFG_RULE_SPAWN_PODS) pmax = ru.i[0];
     if (ru.op == MFG_RULE_SPAWN_DROPOFFS) dropmax = ru.i[0];
     if (ru.op == MFG_RULE_SPAWN_DESTS) destmax = ru.i[0];
+    if (ru.op == MFG_RULE_SPAWN_DEST_ON_AGENT) destmax = s->n_agents;
+    if (ru.op == MFG_RULE_SPAWN_DEST_PER_AGENT) destmax = s->n_dest_entries;
     if (ru.op == MFG_RULE_SPAWN_MACHINES) mmax = ru.i[0];
     if (ru.op == MFG_RULE_SPAWN_MAINTAINERS) kmax = ru.i[0];
     if (ru.op == MFG_RULE_MOVE_MAINTAINERS) moving = 1;
@@ -2834,7 +2980,9 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     h.dirt_cap = (int)std::min<long long>(MFG_DIRT_MAX, std::max<long long>(MFG_WAVE, (need + 63) / 64 * 64));
   }
   // per-wave LDS scratch: spawn positions + amounts of the largest dirt spawn, maintainer routes, >= 2 KB
-  h.scratch_bytes = align_up(std::max({2048, 12 * (dirt_q + 2) + 16, 2 * (h.path_cap + 2)}), 16);
+  int dest_list = 0;  // SpawnDestinationsPerAgent candidate list after the shuffle sinks (quantity mode: the floor)
+  for (int j = 0; j < s->n_dest_entries; j++) dest_list = std::max(dest_list, s->dest_entry_q[j] ? 2 * s->n_floor : 64);
+  h.scratch_bytes = align_up(std::max({2048, 12 * (dirt_q + 2) + 16, 2 * (h.path_cap + 2), 128 + dest_list + 64}), 16);
   make_layout(s, &h.L, imax, pmax, dropmax, destmax, mmax, kmax, h.mstate_ints, h.path_cap, moving, h.dirt_cap);
   h.step_rng = 0;
   for (int r = 0; r < s->n_rules; r++)  // dirt spawns and maintainer retargets consume the floor order mid-step
@@ -2861,7 +3009,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   }
   h.pair_pool = nullptr;
   h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
-  h.fv_words = align_up((2 * h.d + 1) * (2 * h.d + 1), 4);
+  h.fv_words = align_up((2 * h.fr + 1) * (2 * h.fr + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
               8 * h.dd;  // + per-window-cell agent masks (u64)
@@ -2896,7 +3044,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   for (int c = 0; c < HW; c++)
     if (s->level[c] == 1) { base_map[c] = CM_WALL; base_map8[c] = CM_WALL; }
   std::vector<int32_t> wd;
-  const int reach = 2 * s->pomdp_r + 1;
+  const int reach = h.fr;
   for (int k = 0; k < s->n_walls && k < s->n_doors; k++) {
     const int wc = s->wall_cells[k], dc = s->door_cells[k];
     const int dx = wc / s->W - dc / s->W, dy = wc % s->W - dc % s->W;
@@ -2918,7 +3066,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   std::vector<uint32_t> rdiag(h.nrays, 0u);
   for (int r = 0; r < h.nrays; r++) {
     const int p0 = s->ray_off[r], p1 = s->ray_off[r + 1];
-    if (p1 - p0 > h.maxpts) { delete e; return fail("ray longer than 2r+2 points"); }
+    if (p1 - p0 > h.maxpts || p1 - p0 > h.fr + 1) { delete e; return fail("ray longer than its radius + 1 points"); }
     if (p1 - p0 < 1 || s->ray_pts[2 * p0] != 0 || s->ray_pts[2 * p0 + 1] != 0) {  // k_obs relies on it
       delete e; return fail("every ray must start at the origin (bresenham_loop, ray_caster.py:141-199)");
     }
@@ -3058,6 +3206,8 @@ static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
     case 14: { constexpr int MP = 14; CALL; } break; \
     case 16: { constexpr int MP = 16; CALL; } break; \
     case 18: { constexpr int MP = 18; CALL; } break; \
+    case 24: { constexpr int MP = 24; CALL; } break; \
+    case 32: { constexpr int MP = 32; CALL; } break; \
     default: return fail("unsupported ray length"); \
   }
 

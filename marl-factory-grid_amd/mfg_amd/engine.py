@@ -106,6 +106,7 @@ class Engine:
         self.lmax = self.layout['lmax']
         self.A = spec.n_agents
         self.d = spec.d
+        self.obs_hw = tuple(spec.obs_hw)  # (d, d), or the level shape with full observability
 
     def close(self):
         if getattr(self, 'h', None) is not None and self.h.value:
@@ -122,7 +123,7 @@ class Engine:
         return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     def obs_shape(self, K=None):
-        s = (self.B, self.A, self.lmax, self.d, self.d)
+        s = (self.B, self.A, self.lmax) + self.obs_hw
         return s if K is None else (K,) + s
 
     def reset(self, obs=None, mask=None, init=False, seed_base=0):

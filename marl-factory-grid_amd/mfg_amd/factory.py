@@ -128,8 +128,8 @@ class Factory:
     @property
     def observation_space(self):
         _, Tuple, Box = _spaces()
-        d, nl = self.spec.d, self.spec.n_layers
-        boxes = [Box(low=0, high=1, shape=(nl[a], d, d), dtype=np.float32) for a in range(self.spec.n_agents)]
+        hw, nl = tuple(self.spec.obs_hw), self.spec.n_layers
+        boxes = [Box(low=0, high=1, shape=(nl[a],) + hw, dtype=np.float32) for a in range(self.spec.n_agents)]
         return boxes[0] if len(boxes) == 1 else Tuple(boxes)
 
     @property

@@ -49,9 +49,9 @@ class VectorFactory:
         self._ret = self.torch.zeros((self.num_envs, self.n_agents), dtype=self.torch.float64, device=dev)
         self._len = self.torch.zeros(self.num_envs, dtype=self.torch.int64, device=dev)
         Discrete, Tuple, Box = _spaces()
-        d, nl = self.spec.d, self.spec.n_layers
+        hw, nl = tuple(self.spec.obs_hw), self.spec.n_layers
         self.single_action_space = Tuple([Discrete(n) for n in self.spec.n_actions])
-        self.single_observation_space = Tuple([Box(0, 1, (nl[a], d, d), np.float32) for a in range(self.n_agents)])
+        self.single_observation_space = Tuple([Box(0, 1, (nl[a],) + hw, np.float32) for a in range(self.n_agents)])
 
     def reset(self, seed=None, options=None):
         """Create (first call) or reset every env (options={'mask': bool tensor [B]} resets a subset). A
@@ -109,7 +109,7 @@ class ParallelFactory:
     def observation_space(self, agent):
         _, _, Box = _spaces()
         a = self.possible_agents.index(agent)
-        return Box(0, 1, (self.spec.n_layers[a], self.spec.d, self.spec.d), np.float32)
+        return Box(0, 1, (self.spec.n_layers[a],) + tuple(self.spec.obs_hw), np.float32)
 
     def action_space(self, agent):
         Discrete, _, _ = _spaces()
@@ -158,7 +158,7 @@ class SB3VecFactory:
         spec = self.venv.spec
         self._L = max(spec.n_layers)
         _, _, Box = _spaces()
-        self.observation_space = Box(0, 1, (spec.n_agents * self._L, spec.d, spec.d), np.float32)
+        self.observation_space = Box(0, 1, (spec.n_agents * self._L,) + tuple(spec.obs_hw), np.float32)
         self.action_space = _multidiscrete(spec.n_actions)
         self._actions = None
 

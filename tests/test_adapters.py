@@ -25,6 +25,7 @@ class _ScriptedBatched:
 
         class S:
             n_agents, d = A, 3
+            obs_hw = (3, 3)
             n_layers = [2] * A
             n_actions = [5] * A
             agent_names = [f'a{k}' for k in range(A)]

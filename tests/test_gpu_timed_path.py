@@ -138,7 +138,7 @@ def test_output_rows_respect_header_widths():
     G = 4096
     sentinel = 0x5A
     shapes = dict(reward=(K * B * A * 8), done=(K * B), ev_act=(K * B * A), ev_watch=(K * B * A),
-                  ev_misc=(K * B * EV_MISC * 4), obs=(K * B * A * eng.lmax * eng.d * eng.d * 4))
+                  ev_misc=(K * B * EV_MISC * 4), obs=(K * B * A * eng.lmax * eng.obs_hw[0] * eng.obs_hw[1] * 4))
     raw = {k: torch.full((n + G,), sentinel, dtype=torch.uint8, device=eng.device) for k, n in shapes.items()}
     views = dict(reward=raw['reward'][:shapes['reward']].view(torch.float64),
                  done=raw['done'][:shapes['done']], ev_act=raw['ev_act'][:shapes['ev_act']],
