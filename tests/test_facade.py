@@ -47,7 +47,9 @@ def test_no_cpu_fallback():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('tag,cfg', [('large8', 'large8.yaml'), ('rooms4', 'rooms4.yaml'), ('simple1', 'simple1.yaml')])
+@pytest.mark.parametrize('tag,cfg', [('large8', 'large8.yaml'), ('rooms4', 'rooms4.yaml'), ('simple1', 'simple1.yaml'),
+                                     ('eight_puzzle', 'eight_puzzle.yaml'), ('narrow_corridor', 'narrow_corridor.yaml'),
+                                     ('puzzle_dest_crash', 'puzzle_dest_crash.yaml')])
 def test_facade_replays_reference_fixture(tag, cfg):
     if not gpu_available():
         pytest.skip('no GPU')
