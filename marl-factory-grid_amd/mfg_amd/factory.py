@@ -362,5 +362,14 @@ class BatchedFactory:
         return dict(rebuild_info(self.spec, [int(x) for x in actions], ev,
                                  [float(x) for x in self.reward[b].cpu().numpy()]))
 
+    def info_columns(self, actions):
+        """The last step's info dicts of all B envs as device columns (mfg_amd.info_columns): returns
+        (names, values f64 [B, K], present bool [B, K]); no host copy."""
+        if getattr(self, '_info_cols', None) is None:
+            from .info_columns import InfoColumns
+            self._info_cols = InfoColumns(self.spec)
+        v, p = self._info_cols(actions, self.ev_act, self.ev_watch, self.ev_misc, self.reward)
+        return self._info_cols.columns, v, p
+
     def close(self):
         self.engine.close()
