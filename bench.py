@@ -169,6 +169,10 @@ def main():
                     help='obs precision of the headline line (the reference returns f64 obs, Q25)')
     ap.add_argument('--alt-steps', type=int, default=None,
                     help='steps of the second measurement with the other obs dtype (default: --steps; 0 = off)')
+    ap.add_argument('--packed-steps', type=int, default=None,
+                    help='steps of the packed-obs + fused-projection measurement (default: --steps; 0 = off)')
+    ap.add_argument('--cap', type=int, default=32, help='packed entries stored per agent row')
+    ap.add_argument('--emb', type=int, default=96, help='fused projection width (obs_emb_size of RecurrentAC)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-profile', action='store_true', help='no per-kernel HIP events in the timed region')
     args = ap.parse_args()
@@ -248,6 +252,26 @@ def main():
         dist.all_reduce(episodes)  # optional metrics all-reduce (tiny, latency-bound)
     total = B * world * args.steps
     value = total / elapsed
+    def timed(n, obs_buf):
+        """n more steps into obs_buf, timed like the headline (barrier + synchronize brackets, max over ranks)."""
+        run(F, obs_buf=obs_buf)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        run(n, obs_buf=obs_buf)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
     # the same workload with the other obs precision (the reference's own obs are f64, Q25), timed the same way
     alt = None
     alt_steps = args.steps if args.alt_steps is None else args.alt_steps
@@ -255,22 +279,7 @@ def main():
         alt_dtype = 'f32' if args.obs_dtype == 'f64' else 'f64'
         obs_alt = torch.zeros((F,) + eng.obs_shape(), dtype=torch.float64 if alt_dtype == 'f64' else torch.float32,
                               device=dev)
-        run(F, obs_buf=obs_alt)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        run(alt_steps, obs_buf=obs_alt)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        el2 = time.perf_counter() - t1
-        if world > 1:
-            t = torch.tensor([el2], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el2 = float(t.item())
+        el2 = timed(alt_steps, obs_alt)
         alt_obs_bytes = sum(spec.n_layers) * spec.obs_hw[0] * spec.obs_hw[1] * (8 if alt_dtype == 'f64' else 4)
         alt_step_bytes = core_bytes(spec) + alt_obs_bytes
         alt_value = B * world * alt_steps / el2
@@ -279,6 +288,26 @@ def main():
                "pipeline_GBs": round(alt_value / world * alt_step_bytes / 1e9, 2),
                "pipeline_frac": round(alt_value / world * alt_step_bytes / 1e9 / HBM_PEAK_GBS, 5)}
         del obs_alt
+    # packed obs + fused policy-input projection: no dense obs at all
+    packed = None
+    packed_steps = args.steps if args.packed_steps is None else args.packed_steps
+    if packed_steps > 0:
+        from mfg_amd.engine import PackedObs
+        kdim = eng.lmax * eng.obs_hw[0] * eng.obs_hw[1]
+        g = torch.Generator(device=dev).manual_seed(0)
+        w = torch.randn((args.emb, kdim), generator=g, device=dev) * 0.05
+        po = PackedObs(eng, K=F, cap=args.cap, weight=w, bias=torch.zeros(args.emb, device=dev))
+        el3 = timed(packed_steps, po)
+        pk_bytes = core_bytes(spec) + A * (4 + 6 * args.cap + 4 * args.emb)
+        pv = B * world * packed_steps / el3
+        packed = {"obs": f"packed (cap {args.cap}) + fused obs_proj (E {args.emb}, f32)", "value": round(pv, 1),
+                  "unit": "env-steps/s", "steps": packed_steps, "ms_per_step": round(el3 / packed_steps * 1e3, 4),
+                  "algo_bytes_per_env_step": pk_bytes,
+                  "pipeline_GBs": round(pv / world * pk_bytes / 1e9, 2),
+                  "max_row_nnz": int(po.count.max()),
+                  "dense_f32_bytes_per_env_step": core_bytes(spec) + sum(spec.n_layers) * spec.obs_hw[0] *
+                  spec.obs_hw[1] * 4}
+        del po
     if rank == 0:
         full = [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls if k == F] or \
                [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls]
@@ -373,6 +402,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "alt_obs_dtype": alt,
+            "packed_obs": packed,
         }
         print(json.dumps(out))
     eng.close()

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MFG_ABI_VERSION 2
+#define MFG_ABI_VERSION 3
 
 #define MFG_MAX_AGENTS 64
 #define MFG_MAX_ACTIONS 16
@@ -230,6 +230,34 @@ typedef struct mfg_events {
 int mfg_decode_events(const uint8_t* ev_act, const uint8_t* ev_watch, const int32_t* ev_misc, int n_agents,
                       mfg_events* out);
 
+/* ---- observation output modes (the obs_dtype argument of mfg_reset / mfg_step) ---- */
+enum { MFG_OBS_F32 = 0, MFG_OBS_F64 = 1, MFG_OBS_PACKED = 2 };
+#define MFG_MAX_EMB 256
+
+/* Packed observations + fused policy-input projection. With obs_dtype MFG_OBS_PACKED the
+ * `obs` argument is a HOST pointer to this descriptor; its device buffers are the k = 0 rows and the engine
+ * offsets them per fused step. Per agent row (the dense row [lmax][h][w] of MFG_OBS_F32, whose values are
+ * the reference's f64 obs cast like `observations.float()` in algorithms/marl/networks.py:52):
+ *   count[a]       number of nonzero entries of the dense row (may exceed cap: only cap are stored)
+ *   idx/val[a][i]  the nonzero entries, i < min(count, cap): flat index l*h*w + cell and the value, in
+ *                  (64-cell block, layer, cell) order, i.e. ascending idx when h*w <= 64; slots >= count are
+ *                  written as idx 0 / val 0, so a fixed-width gather over all cap slots is exact
+ *   emb[a][j]      bias[j] + sum over ALL nonzero entries of val * wt[idx][j] (f32 fma in entry order): the
+ *                  reference RecurrentAC.obs_proj (networks.py:19,52) evaluated without materialising the
+ *                  dense row. wt = obs_proj.weight transposed, [lmax*h*w][emb_dim] row-major.
+ * Any of idx/val (both or neither), count and emb may be NULL; emb needs wt and 0 < emb_dim <= MFG_MAX_EMB.
+ * lmax*h*w must be < 65536 (u16 idx). */
+typedef struct mfg_packed_obs {
+  int32_t cap;        /* entries stored per agent row */
+  int32_t emb_dim;    /* E; 0 = no projection */
+  uint16_t* idx;      /* [K][B][A][cap] */
+  float* val;         /* [K][B][A][cap] */
+  int32_t* count;     /* [K][B][A] */
+  const float* wt;    /* [lmax*h*w][E] */
+  const float* bias;  /* [E] or NULL (zeros) */
+  float* emb;         /* [K][B][A][E] */
+} mfg_packed_obs;
+
 /* ---- engine ABI (HIP) ---- */
 typedef struct mfg_engine mfg_engine;
 
@@ -252,7 +280,7 @@ const char* mfg_last_error(const mfg_engine* e);
  * §8c seeding contract), or, with MFG_INIT_KEEP_MT, keeps the MT19937 state + index already imported
  * into its record (mfg_import_state), e.g. the caller's Python `random` state. MFG_INIT_NO_RESET stops
  * after creation (the reference's constructor does not reset). obs (device, may be NULL):
- * [B][A][lmax][d][d], obs_dtype 0 = float32, 1 = float64. */
+ * [B][A][lmax][d][d], obs_dtype 0 = float32, 1 = float64; or MFG_OBS_PACKED with obs -> mfg_packed_obs. */
 enum { MFG_INIT_CREATE = 1, MFG_INIT_KEEP_MT = 2, MFG_INIT_NO_RESET = 4 };
 int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init, uint64_t seed_base,
               void* stream);
@@ -261,7 +289,9 @@ int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int 
  * actions: device int32 [K][B][A] indices into each agent's action list, or NULL for synthetic uniform
  * actions from Philox4x32-10 keyed (philox_seed, env_base + b) at counter (step_base + k, agent).
  * Outputs (device, each may be NULL): reward f64 [K][B][A], done u8 [K][B], obs [K][B][A][lmax][h][w]
- * (h = w = 2 pomdp_r + 1, or the level's H x W when pomdp_r == 0), ev_act / ev_watch u8 [K][B][A] and
+ * (h = w = 2 pomdp_r + 1, or the level's H x W when pomdp_r == 0) in obs_dtype MFG_OBS_F32 / MFG_OBS_F64, or
+ * the packed rows + fused projection of an mfg_packed_obs descriptor (obs_dtype MFG_OBS_PACKED; obs = host pointer),
+ * ev_act / ev_watch u8 [K][B][A] and
  * ev_misc i32 [K][B][MFG_EV_MISC_N] (the info-dict event rows above).
  * An action index outside [0, n_actions[a]) crashes that env (MFG_CRASH_ACTION, done = 1).
  * auto_reset != 0: an env whose step is done is reset before its obs row is rendered, so the row is the

@@ -2055,8 +2055,19 @@ __device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
   }
 }
 
-template <int MAXPTS, typename OT, bool MM>
-__device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
+// packed obs rows + fused projection of one env (mfg_packed_obs, include/mfg.h), offset to this env
+struct ObsPacked {
+  uint16_t* idx;
+  float* val;
+  int* cnt;
+  const float* wt;
+  const float* bias;
+  float* emb;
+  int cap, E;
+};
+
+template <int MAXPTS, typename OT, bool MM, bool PK>
+__device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPacked& pk) {
   SpecP S = e.S;
   // window: oh x ow cells from (wx0, wy0) = agent - r, or the whole level at (0, 0) when pomdp_r == 0
   // (observation_builder.py:152-158); rays and the first-visit table have radius fr (Q13)
@@ -2181,8 +2192,18 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
       }
     }
     wave_sync();
-    OT* out_a = out_env + (size_t)a * S->obs_agent_stride;
+    OT* out_a = PK ? nullptr : out_env + (size_t)a * S->obs_agent_stride;
     const int nl = S->s.n_layers[a];
+    // packed mode: entry count so far and the projection accumulators (lane j holds outputs j, 64 + j, ...)
+    int pcount = 0;
+    float acc[MFG_MAX_EMB / MFG_WAVE];
+    if constexpr (PK) {
+#pragma unroll
+      for (int q = 0; q < MFG_MAX_EMB / MFG_WAVE; q++) {
+        const int j = q * MFG_WAVE + lane;
+        acc[q] = (pk.bias && j < pk.E) ? pk.bias[j] : 0.0f;
+      }
+    }
     // ---- placement (lane = window cell, 64 cells per pass): tag bits from the cell map ----
 #ifdef MFG_ABLATE_OB_NOPLACE
     if (0)
@@ -2280,6 +2301,35 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
           }
           out = (OT)val;
         }
+        if constexpr (PK) {
+          // nonzero entries of this layer's 64-cell block, in lane order; the projection walks them in
+          // the same order (uniform loop, lane = output feature, coalesced rows of wt)
+          const float fv = (float)out;
+          const bool nz = inwin && fv != 0.0f;
+          const u64 nzm = ballot(nz);
+          const int base = l * dd + w0;
+          if (pk.idx) {
+            const int pos = pcount + mbcnt(nzm);
+            if (nz && pos < pk.cap) {
+              pk.idx[(size_t)a * pk.cap + pos] = (uint16_t)(base + lane);
+              pk.val[(size_t)a * pk.cap + pos] = fv;
+            }
+          }
+          pcount += popc(nzm);
+          if (pk.emb) {
+            for (u64 m = nzm; m; m &= m - 1) {
+              const int b = ffs64(m);
+              const float v = __int_as_float(rl(__float_as_int(fv), b));
+              const float* wr = pk.wt + (size_t)(base + b) * pk.E;
+#pragma unroll
+              for (int q = 0; q < MFG_MAX_EMB / MFG_WAVE; q++) {
+                const int j = q * MFG_WAVE + lane;
+                if (q * MFG_WAVE < pk.E && j < pk.E) acc[q] = __builtin_fmaf(v, wr[j], acc[q]);
+              }
+            }
+          }
+          continue;
+        }
         // non-temporal: the obs stream is not re-read by this GPU (k_obs 0.500 -> 0.493 ms, k_logic
         // 0.298 -> 0.291 ms at C3: less L2 pollution). WRITE_SIZE counts 1.34x the algorithmic obs bytes
         // for these stores (1.00x with MFG_OBS_NT=0): the 49-lane layer rows are not 64-B aligned.
@@ -2290,6 +2340,21 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob) {
 #else
         if (inwin) out_a[(size_t)l * dd + wi] = out;
 #endif
+      }
+    }
+    if constexpr (PK) {
+      if (pk.idx)  // unused slots: idx 0 / val 0 (a fixed-width gather over the row stays exact)
+        for (int i = pcount + lane; i < pk.cap; i += MFG_WAVE) {
+          pk.idx[(size_t)a * pk.cap + i] = 0;
+          pk.val[(size_t)a * pk.cap + i] = 0.0f;
+        }
+      if (pk.cnt && lane == 0) pk.cnt[a] = pcount;
+      if (pk.emb) {
+#pragma unroll
+        for (int q = 0; q < MFG_MAX_EMB / MFG_WAVE; q++) {
+          const int j = q * MFG_WAVE + lane;
+          if (q * MFG_WAVE < pk.E && j < pk.E) pk.emb[(size_t)a * pk.E + j] = acc[q];
+        }
       }
     }
   }
@@ -2517,9 +2582,9 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_
 
 // Observation render of every env into obs[env] (read-only on the state). MM: the spec has machines or
 // maintainers (their tags, identifiers and dedupe); compiled out otherwise to keep the VGPR budget.
-template <int MAXPTS, typename OT, bool MM>
+template <int MAXPTS, typename OT, bool MM, bool PK>
 __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
-                                                      OT* obs) {
+                                                      OT* obs, ObsPacked pk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = uni(threadIdx.x >> 6);  // wave-uniform: slice and record addresses become scalar
@@ -2537,7 +2602,16 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, cons
   rec_copy(e.lds, rec, S->L.o_mt, e.lane);
   wave_sync();
   int* pg = S->pair_pool ? S->pair_pool + (size_t)env * 3 * (S->max_pairs - S->pairs_lds) : nullptr;
-  build_obs<MAXPTS, OT, MM>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg);
+  if constexpr (PK) {  // this env's rows of the packed buffers
+    const size_t ea = (size_t)env * S->A;
+    pk.idx = pk.idx ? pk.idx + ea * pk.cap : nullptr;
+    pk.val = pk.val ? pk.val + ea * pk.cap : nullptr;
+    pk.cnt = pk.cnt ? pk.cnt + ea : nullptr;
+    pk.emb = pk.emb ? pk.emb + ea * pk.E : nullptr;
+    build_obs<MAXPTS, OT, MM, PK>(e, nullptr, pg, pk);
+  } else {
+    build_obs<MAXPTS, OT, MM, PK>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg, pk);
+  }
   if (e.lane == 0 && e.hdrp[H_OVERFLOW]) ((int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_OVERFLOW] = 1;
 }
 
@@ -3185,14 +3259,14 @@ static unsigned env_grid(const mfg_engine* e, int wpb) { return (unsigned)((e->B
 // launch geometry of a kernel with `lds` bytes of dynamic LDS per wave
 #define GEOM(lds) dim3(env_grid(e, wpb_for(lds))), dim3(wpb_for(lds) * 64), (size_t)(lds) * wpb_for(lds)
 
-template <int MP, typename OT>
-static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
+template <int MP, typename OT, bool PK>
+static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipStream_t st) {
   if (e->h.mmax || e->h.kmax)
-    hipLaunchKernelGGL((k_obs<MP, OT, true>), GEOM(e->h.lds_obs),
-                       st, e->d_spec, e->d_state, (long long)e->B, obs);
+    hipLaunchKernelGGL((k_obs<MP, OT, true, PK>), GEOM(e->h.lds_obs),
+                       st, e->d_spec, e->d_state, (long long)e->B, obs, pk);
   else
-    hipLaunchKernelGGL((k_obs<MP, OT, false>), GEOM(e->h.lds_obs),
-                       st, e->d_spec, e->d_state, (long long)e->B, obs);
+    hipLaunchKernelGGL((k_obs<MP, OT, false, PK>), GEOM(e->h.lds_obs),
+                       st, e->d_spec, e->d_state, (long long)e->B, obs, pk);
   return hipGetLastError();
 }
 
@@ -3211,14 +3285,43 @@ static hipError_t launch_obs_t(mfg_engine* e, OT* obs, hipStream_t st) {
     default: return fail("unsupported ray length"); \
   }
 
-// render obs of every env into obs (obs_dtype 0 = f32, 1 = f64)
-static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st) {
+// check a packed-obs descriptor (host memory) against the engine: returns 0 or fails
+static int check_packed(const mfg_engine* e, const mfg_packed_obs* p) {
+  if (!p) return fail("MFG_OBS_PACKED needs an mfg_packed_obs descriptor");
+  if ((p->idx == nullptr) != (p->val == nullptr)) return fail("packed obs: idx and val must both be set or both NULL");
+  if (p->idx && p->cap <= 0) return fail("packed obs: cap must be > 0 when idx/val are given");
+  if (p->emb && (p->emb_dim <= 0 || p->emb_dim > MFG_MAX_EMB || !p->wt))
+    return fail("packed obs: emb needs wt and 0 < emb_dim <= MFG_MAX_EMB");
+  if ((size_t)e->h.obs_agent_stride > 65535) return fail("packed obs: lmax*h*w >= 65536 does not fit the u16 idx");
+  return 0;
+}
+// the k-th fused step's rows of a packed-obs descriptor
+static ObsPacked packed_rows(const mfg_engine* e, const mfg_packed_obs* p, int k) {
+  const size_t ba = (size_t)k * (size_t)e->B * (size_t)e->h.A;
+  ObsPacked pk;
+  pk.cap = p->idx ? p->cap : 0;
+  pk.E = p->emb ? p->emb_dim : 0;
+  pk.idx = p->idx ? p->idx + ba * pk.cap : nullptr;
+  pk.val = p->val ? p->val + ba * pk.cap : nullptr;
+  pk.cnt = p->count ? p->count + ba : nullptr;
+  pk.wt = p->wt;
+  pk.bias = p->bias;
+  pk.emb = p->emb ? p->emb + ba * pk.E : nullptr;
+  return pk;
+}
+
+// render obs of every env into obs (obs_dtype 0 = f32, 1 = f64, 2 = packed: obs -> mfg_packed_obs, row k)
+static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st, int k = 0) {
   hipError_t err = hipSuccess;
   PROF_BEGIN(e, st);
-  if (obs_dtype == 1) {
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double>(e, (double*)obs, st)));
+  ObsPacked none{};
+  if (obs_dtype == MFG_OBS_PACKED) {
+    const ObsPacked pk = packed_rows(e, (const mfg_packed_obs*)obs, k);
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, true>(e, (float*)nullptr, pk, st)));
+  } else if (obs_dtype == MFG_OBS_F64) {
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double, false>(e, (double*)obs, none, st)));
   } else {
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float>(e, (float*)obs, st)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, false>(e, (float*)obs, none, st)));
   }
   if (err != hipSuccess) return fail(std::string("k_obs launch: ") + hipGetErrorString(err));
   PROF_END(e, st, MFG_K_OBS);
@@ -3235,7 +3338,9 @@ extern "C" int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_
 }
 static int reset_impl(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int init, uint64_t seed_base,
                       void* stream) {
-  if (obs_dtype != 0 && obs_dtype != 1) return fail("obs_dtype must be 0 (f32) or 1 (f64)");
+  if (obs && obs_dtype != MFG_OBS_F32 && obs_dtype != MFG_OBS_F64 && obs_dtype != MFG_OBS_PACKED)
+    return fail("obs_dtype must be MFG_OBS_F32, MFG_OBS_F64 or MFG_OBS_PACKED");
+  if (obs && obs_dtype == MFG_OBS_PACKED && check_packed(e, (const mfg_packed_obs*)obs)) return -1;
   hipStream_t st = (hipStream_t)stream;
   PROF_BEGIN(e, st);
   hipLaunchKernelGGL(k_reset, GEOM(e->h.lds_full), st, e->d_spec,
@@ -3279,10 +3384,12 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
                      int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
                      uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
   if (K < 1) return fail("K must be >= 1");
-  if (obs && obs_dtype != 0 && obs_dtype != 1) return fail("obs_dtype must be 0 (f32) or 1 (f64)");
+  if (obs && obs_dtype != MFG_OBS_F32 && obs_dtype != MFG_OBS_F64 && obs_dtype != MFG_OBS_PACKED)
+    return fail("obs_dtype must be MFG_OBS_F32, MFG_OBS_F64 or MFG_OBS_PACKED");
+  if (obs && obs_dtype == MFG_OBS_PACKED && check_packed(e, (const mfg_packed_obs*)obs)) return -1;
   hipStream_t st = (hipStream_t)stream;
   const size_t B = (size_t)e->B, A = (size_t)e->h.A;
-  const size_t obs_row = B * A * (size_t)e->h.obs_agent_stride * (obs_dtype == 1 ? 8 : 4);
+  const size_t obs_row = B * A * (size_t)e->h.obs_agent_stride * (obs_dtype == MFG_OBS_F64 ? 8 : 4);
   for (int k = 0; k < K; k++) {
     const size_t kb = (size_t)k * B;
     {
@@ -3322,7 +3429,9 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
       PROF_END(e, st, MFG_K_RESETDONE);
     }
 #ifndef MFG_ABLATE_NOOBS
-    if (obs && launch_obs(e, (uint8_t*)obs + (size_t)k * obs_row, obs_dtype, st)) return -1;
+    if (obs && obs_dtype == MFG_OBS_PACKED && launch_obs(e, obs, obs_dtype, st, k)) return -1;
+    if (obs && obs_dtype != MFG_OBS_PACKED && launch_obs(e, (uint8_t*)obs + (size_t)k * obs_row, obs_dtype, st))
+      return -1;
 #endif
   }
   return replay_impl(e, stream);

@@ -33,7 +33,7 @@ LAYER_ZERO, LAYER_TAG, LAYER_COMBINED, LAYER_BATTERY, LAYER_GLOBALPOS = range(5)
 
 DEST_ANY, DEST_ALL, DEST_SIMULTANEOUS = range(3)
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 # ev_misc row (include/mfg.h MFG_EVM_*)
 EV_MISC_N = 12
 (EVM_DOOR_COLL_LO, EVM_DOOR_COLL_HI, EVM_RESPAWN_ITEMS, EVM_DIRT_SPAWN, EVM_DIRT_VALID, EVM_DEST_REACHED, EVM_FLAGS,
@@ -123,4 +123,22 @@ class MfgEvents(C.Structure):
         ('step', C.c_int32),
         ('episode', C.c_int32),
         ('maint_base', C.c_int32),
+    ]
+
+
+# observation output modes (include/mfg.h MFG_OBS_*) and the packed-obs descriptor
+OBS_F32, OBS_F64, OBS_PACKED = range(3)
+MAX_EMB = 256
+
+
+class MfgPackedObs(C.Structure):
+    _fields_ = [
+        ('cap', C.c_int32),
+        ('emb_dim', C.c_int32),
+        ('idx', C.c_void_p),
+        ('val', C.c_void_p),
+        ('count', C.c_void_p),
+        ('wt', C.c_void_p),
+        ('bias', C.c_void_p),
+        ('emb', C.c_void_p),
     ]

@@ -126,16 +126,26 @@ class Engine:
         s = (self.B, self.A, self.lmax) + self.obs_hw
         return s if K is None else (K,) + s
 
+    def _obs_arg(self, obs, K):
+        """(pointer, obs_dtype) of a dense obs tensor or a PackedObs (MFG_OBS_PACKED: host descriptor)."""
+        if isinstance(obs, PackedObs):
+            if obs.engine is not self or obs.K < K:
+                raise ValueError('PackedObs was made for another engine or fewer fused steps')
+            return C.byref(obs.desc), abi.OBS_PACKED
+        if obs is not None and not obs.is_contiguous():
+            raise ValueError('obs must be contiguous')
+        return _ptr(obs), (abi.OBS_F64 if (obs is not None and obs.dtype == self.torch.float64) else abi.OBS_F32)
+
     def reset(self, obs=None, mask=None, init=False, seed_base=0):
-        dt = 1 if (obs is not None and obs.dtype == self.torch.float64) else 0
-        _check(self.L.mfg_reset(self.h, _ptr(mask), _ptr(obs), dt, int(init), int(seed_base), self._stream()),
+        op, dt = self._obs_arg(obs, 1)
+        _check(self.L.mfg_reset(self.h, _ptr(mask), op, dt, int(init), int(seed_base), self._stream()),
                'mfg_reset', self.h)
 
     def step(self, K=1, actions=None, philox_seed=0, env_base=0, step_base=0, reward=None, done=None, obs=None,
              ev_act=None, ev_watch=None, ev_misc=None, auto_reset=True):
-        dt = 1 if (obs is not None and obs.dtype == self.torch.float64) else 0
+        op, dt = self._obs_arg(obs, K)
         _check(self.L.mfg_step(self.h, int(K), _ptr(actions), int(philox_seed) & 0xFFFFFFFF, int(env_base),
-                               int(step_base), _ptr(reward), _ptr(done), _ptr(obs), dt, _ptr(ev_act),
+                               int(step_base), _ptr(reward), _ptr(done), op, dt, _ptr(ev_act),
                                _ptr(ev_watch), _ptr(ev_misc), int(bool(auto_reset)), self._stream()), 'mfg_step',
                self.h)
 
@@ -160,6 +170,84 @@ class Engine:
     def import_state(self, t):
         assert t.dtype == self.torch.uint8 and t.numel() == self.B * self.layout['size']
         _check(self.L.mfg_import_state(self.h, _ptr(t.contiguous()), self._stream()), 'mfg_import_state')
+
+
+class PackedObs:
+    """Device buffers of the packed observation mode (MFG_OBS_PACKED, `mfg_packed_obs` in include/mfg.h) for
+    K fused steps, SURVEY §8(f) f3. Per (step, env, agent) row of the dense obs [lmax, h, w]:
+
+    * ``idx`` u16 / ``val`` f32 [K, B, A, cap]: the nonzero entries (flat index ``l*h*w + cell``, value as
+      ``observations.float()`` in the reference network, algorithms/marl/networks.py:52); slots past the count
+      are 0 / 0.0, so a fixed-width gather over all ``cap`` slots is exact;
+    * ``count`` i32 [K, B, A]: the true number of nonzero entries (``> cap`` = truncated row, see ``check()``);
+    * ``emb`` f32 [K, B, A, E]: ``bias + sum val * weight[:, idx]``, the reference ``RecurrentAC.obs_proj``
+      (networks.py:19) fused into the render, over ALL nonzero entries.
+
+    ``weight`` is an ``nn.Linear(lmax*h*w, E).weight`` ([E, lmax*h*w]); ``set_projection`` refreshes the
+    engine's transposed copy after an optimizer step (same device pointers, no reallocation)."""
+
+    def __init__(self, engine, K=1, cap=32, weight=None, bias=None, entries=True, count=True):
+        torch = engine.torch
+        self.engine, self.K, self.cap = engine, int(K), int(cap) if entries else 0
+        B, A = engine.B, engine.A
+        self.kdim = engine.lmax * engine.obs_hw[0] * engine.obs_hw[1]
+        dev = engine.device
+        self.idx = torch.zeros((K, B, A, self.cap), dtype=torch.uint16, device=dev) if entries else None
+        self.val = torch.zeros((K, B, A, self.cap), dtype=torch.float32, device=dev) if entries else None
+        self.count = torch.zeros((K, B, A), dtype=torch.int32, device=dev) if count else None
+        self.E = 0
+        self.wt = self.bias = self.emb = None
+        if weight is not None:
+            E = int(weight.shape[0])
+            if not 0 < E <= abi.MAX_EMB or int(weight.shape[1]) != self.kdim:
+                raise ValueError(f'projection weight must be [E <= {abi.MAX_EMB}, {self.kdim}]')
+            self.E = E
+            self.wt = torch.empty((self.kdim, E), dtype=torch.float32, device=dev)
+            self.bias = torch.zeros(E, dtype=torch.float32, device=dev)
+            self.emb = torch.zeros((K, B, A, E), dtype=torch.float32, device=dev)
+            self.set_projection(weight, bias)
+        self.desc = self._make_desc()
+
+    def _make_desc(self):
+        d = abi.MfgPackedObs()
+        d.cap, d.emb_dim = self.cap, self.E
+        for f in ('idx', 'val', 'count', 'wt', 'bias', 'emb'):
+            t = getattr(self, f)
+            setattr(d, f, t.data_ptr() if t is not None else None)
+        return d
+
+    def view(self, k):
+        """Row k as a K = 1 PackedObs sharing this one's buffers (e.g. one slot of a rollout window)."""
+        v = PackedObs.__new__(PackedObs)
+        v.engine, v.K, v.cap, v.kdim, v.E = self.engine, 1, self.cap, self.kdim, self.E
+        for f in ('idx', 'val', 'count', 'emb'):
+            t = getattr(self, f)
+            setattr(v, f, t[k:k + 1] if t is not None else None)
+        v.wt, v.bias = self.wt, self.bias
+        v.desc = v._make_desc()
+        return v
+
+    def set_projection(self, weight, bias=None):
+        """Copy an nn.Linear weight [E, kdim] (and bias [E]) into the engine's transposed f32 buffers."""
+        with self.engine.torch.no_grad():
+            self.wt.copy_(weight.detach().t())
+            if bias is None:
+                self.bias.zero_()
+            else:
+                self.bias.copy_(bias.detach())
+
+    def check(self):
+        """Raise if a stored row was truncated (count > cap); one device->host sync."""
+        if self.count is not None and self.cap and int(self.count.max()) > self.cap:
+            raise RuntimeError(f'packed obs row has {int(self.count.max())} nonzero entries > cap {self.cap}')
+
+    def dense(self, k=0):
+        """Scatter row k back into a dense f32 obs [B, A, lmax, h, w] (test / debugging view)."""
+        torch = self.engine.torch
+        B, A = self.engine.B, self.engine.A
+        out = torch.zeros((B, A, self.kdim), dtype=torch.float32, device=self.engine.device)
+        out.scatter_add_(2, self.idx[k].long(), self.val[k])
+        return out.view((B, A, self.engine.lmax) + self.engine.obs_hw)
 
 
 class RecordView:

@@ -19,7 +19,7 @@ import random as _pyrandom
 import numpy as np
 
 from . import abi
-from .engine import Engine, RecordView, events_from_rows, EV_MISC, HDR, HDR_N
+from .engine import Engine, PackedObs, RecordView, events_from_rows, EV_MISC, HDR, HDR_N
 from .info import rebuild_info
 from .spec import compile_spec, UnsupportedSpec
 from . import views as _views
@@ -307,7 +307,11 @@ class ManualResult:
 class BatchedFactory:
     """B envs of one config on one GPU: torch tensors in and out, auto-reset."""
 
-    def __init__(self, config_file, n_envs, *, device=0, seed_base=0, obs_dtype='float32', custom_level_path=None):
+    def __init__(self, config_file, n_envs, *, device=0, seed_base=0, obs_dtype='float32', custom_level_path=None,
+                 packed_cap=32, proj_weight=None, proj_bias=None):
+        """obs_dtype 'float32' / 'float64': dense obs [B, A, lmax, h, w]; 'packed': an engine.PackedObs
+        (nonzero entries per agent row, cap `packed_cap`, plus the fused projection when `proj_weight`, an
+        nn.Linear(lmax*h*w, E).weight, is given)."""
         import torch
         self.torch = torch
         self.spec = compile_spec(config_file, custom_level_path)
@@ -316,8 +320,11 @@ class BatchedFactory:
         self.device = self.engine.device
         self.seed_base = int(seed_base)
         A = self.spec.n_agents
-        dt = {'float32': torch.float32, 'float64': torch.float64}[obs_dtype]
-        self.obs = torch.zeros(self.engine.obs_shape(), dtype=dt, device=self.device)
+        if obs_dtype == 'packed':
+            self.obs = PackedObs(self.engine, K=1, cap=packed_cap, weight=proj_weight, bias=proj_bias)
+        else:
+            dt = {'float32': torch.float32, 'float64': torch.float64}[obs_dtype]
+            self.obs = torch.zeros(self.engine.obs_shape(), dtype=dt, device=self.device)
         self.reward = torch.zeros((self.B, A), dtype=torch.float64, device=self.device)
         self.done = torch.zeros(self.B, dtype=torch.uint8, device=self.device)
         self.ev_act = torch.zeros((self.B, A), dtype=torch.uint8, device=self.device)

@@ -1,0 +1,292 @@
+"""On-GPU MARL training over the batched engine: packed observations gathered straight
+into the policy input, rollouts and A2C updates without a host round trip.
+
+Reference anchors:
+  * the network: ``algorithms/marl/networks.py:7-69`` ``RecurrentAC`` (same constructor, parameter names and
+    layers, so its ``state_dict`` loads either way);
+  * the loss: ``algorithms/marl/base_ac.py:185-226`` ``compute_advantages`` / ``actor_critic`` / ``learn``
+    (RMSprop lr 3e-4 eps 1e-5, ``clip_grad_norm_(0.5)``, ``base_ac.py:45-47,219-225``);
+  * the loop: ``base_ac.py:90-150`` ``train_loop`` (act on ``(obs, last_action, hidden)``, learn every
+    ``n_steps``), batched over B envs x A agents, one shared network (``snac.py:8-33``).
+
+What is different from the reference, and why:
+  * The obs never exist densely. The engine renders each agent's row as packed nonzero entries plus the fused
+    projection ``obs_proj(obs.float())`` (``mfg_packed_obs``, include/mfg.h); acting reads that projection,
+    learning re-evaluates ``obs_proj`` on the stored entries with ``F.embedding_bag`` (the same sum over the
+    nonzero terms, differentiable in the weight). C3 moves ~6 B x 32 entries per agent row instead of
+    1,372 B of dense f32.
+  * The memory is aligned: entry t holds (o_t, a_{t-1}) as the network input and a_t, r_t, d_t as targets.
+    ``train_loop`` stores the obs of the step *before* each action (``base_ac.py:119``), so its loss pairs
+    a_t with o_{t-1}; the loss function itself (``actor_critic``) is used unchanged and is pinned by a
+    fixture produced by the reference (tests/golden/marl_a2c.npz, tools/gen_golden_marl.py).
+  * Episodes end per env (auto-reset): an entry whose previous step was done starts a new episode, so its
+    action input is -1 (padding) and the recurrent state restarts from zero, as the reference does at every
+    ``env.reset()`` (``base_ac.py:98-100``). The reference's GRU runs the window in one ``nn.GRU`` call;
+    here the same parameters run as GEMMs step by step (input gates for all steps in one GEMM) so the
+    restart can happen inside a window (identical when no episode starts in it, up to f32 rounding).
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.distributions import Categorical
+
+
+class RecurrentAC(nn.Module):
+    """``algorithms/marl/networks.py:7-69`` with the same parameters; adds the packed-obs projection and a
+    step-wise recurrent pass with episode restarts."""
+
+    def __init__(self, observation_size, n_actions, obs_emb_size, action_emb_size, hidden_size_actor,
+                 hidden_size_critic, n_agents, use_agent_embedding=True):
+        super().__init__()
+        observation_size = int(np.prod(observation_size))
+        self.n_layers = 1
+        self.n_actions = n_actions
+        self.use_agent_embedding = use_agent_embedding
+        self.hidden_size_actor = hidden_size_actor
+        self.hidden_size_critic = hidden_size_critic
+        self.action_emb_size = action_emb_size
+        self.obs_proj = nn.Linear(observation_size, obs_emb_size)
+        self.action_emb = nn.Embedding(n_actions + 1, action_emb_size, padding_idx=0)
+        self.agent_emb = nn.Embedding(n_agents, action_emb_size)
+        # networks.py:22 sizes the mix input as obs + n_agents * action_emb with the agent embedding (only
+        # consistent for n_agents == 2); kept so reference checkpoints load
+        mix_in_size = obs_emb_size + action_emb_size if not use_agent_embedding else \
+            obs_emb_size + n_agents * action_emb_size
+        self.mix = nn.Sequential(nn.Tanh(), nn.Linear(mix_in_size, obs_emb_size), nn.Tanh(),
+                                 nn.Linear(obs_emb_size, obs_emb_size))
+        self.gru_actor = nn.GRU(obs_emb_size, hidden_size_actor, batch_first=True, num_layers=self.n_layers)
+        self.gru_critic = nn.GRU(obs_emb_size, hidden_size_critic, batch_first=True, num_layers=self.n_layers)
+        self.action_head = nn.Sequential(nn.Linear(hidden_size_actor, hidden_size_actor), nn.Tanh(),
+                                         nn.Linear(hidden_size_actor, n_actions))
+        self.critic_head = nn.Sequential(nn.Linear(hidden_size_critic, hidden_size_critic), nn.Tanh(),
+                                         nn.Linear(hidden_size_critic, 1))
+
+    def init_hidden_actor(self):
+        return torch.zeros(1, self.n_layers, self.hidden_size_actor)
+
+    def init_hidden_critic(self):
+        return torch.zeros(1, self.n_layers, self.hidden_size_critic)
+
+    # ---- the reference forward (dense obs), networks.py:50-69 ----
+    def forward(self, observations, actions, hidden_actor=None, hidden_critic=None):
+        n, t = observations.shape[:2]
+        obs_emb = self.obs_proj(observations.reshape(n, t, -1).float())
+        agent_ids = torch.arange(n, device=obs_emb.device)
+        return self.forward_emb(obs_emb, actions, hidden_actor, hidden_critic, agent_ids=agent_ids)
+
+    # ---- packed obs -> obs_proj output ----
+    def project_packed(self, idx, val):
+        """obs_proj(obs.float()) from packed rows: idx u16 / val f32 [..., cap] -> [..., obs_emb_size]."""
+        lead = idx.shape[:-1]
+        cap = idx.shape[-1]
+        out = F.embedding_bag(idx.reshape(-1, cap).long(), self.obs_proj.weight.t(),
+                              per_sample_weights=val.reshape(-1, cap), mode='sum')
+        return (out + self.obs_proj.bias).reshape(*lead, -1)
+
+    def forward_emb(self, obs_emb, actions, hidden_actor, hidden_critic, agent_ids=None, starts=None):
+        """obs_emb [N, T, E] (obs_proj output), actions [N, T] (last action, -1 = none), hidden [N, 1, H].
+        starts [N, T] bool: the recurrent state restarts from zero at these entries (episode starts)."""
+        n, t = obs_emb.shape[:2]
+        action_emb = self.action_emb(actions + 1)  # shift by one: padding idx (networks.py:53)
+        if not self.use_agent_embedding:
+            x_t = torch.cat((obs_emb, action_emb), -1)
+        else:
+            ids = agent_ids if agent_ids is not None else torch.arange(n, device=obs_emb.device)
+            agent_emb = self.agent_emb(ids.view(-1, 1).expand(n, t))
+            x_t = torch.cat((obs_emb, agent_emb, action_emb), -1)
+        mixed = self.mix(x_t)
+        ha = hidden_actor[:, 0]
+        hc = hidden_critic[:, 0]
+        keep = None if starts is None else (~starts).to(mixed.dtype)  # [N, T]
+        # the GRU input projections of all T steps as one GEMM each, then the recurrence step by step
+        # (nn.GRU semantics, torch's gate order r, z, n); plain GEMMs instead of the library RNN kernel
+        gi_a = F.linear(mixed, self.gru_actor.weight_ih_l0, self.gru_actor.bias_ih_l0)
+        gi_c = F.linear(mixed, self.gru_critic.weight_ih_l0, self.gru_critic.bias_ih_l0)
+        ps, cs = [], []
+        for s in range(t):
+            if keep is not None:
+                ha = ha * keep[:, s:s + 1]
+                hc = hc * keep[:, s:s + 1]
+            ha = _gru_cell(gi_a[:, s], ha, self.gru_actor)
+            hc = _gru_cell(gi_c[:, s], hc, self.gru_critic)
+            ps.append(ha)
+            cs.append(hc)
+        out_p, out_c = torch.stack(ps, 1), torch.stack(cs, 1)
+        logits = self.action_head(out_p)
+        critic = self.critic_head(out_c).squeeze(-1)
+        return dict(logits=logits, critic=critic, hidden_actor=out_p, hidden_critic=out_c)
+
+
+def _gru_cell(gi, h, gru):
+    """One nn.GRU step (layer 0) from precomputed input gates gi = x W_ih^T + b_ih."""
+    gh = F.linear(h, gru.weight_hh_l0, gru.bias_hh_l0)
+    i_r, i_z, i_n = gi.chunk(3, -1)
+    h_r, h_z, h_n = gh.chunk(3, -1)
+    r = torch.sigmoid(i_r + h_r)
+    z = torch.sigmoid(i_z + h_z)
+    n = torch.tanh(i_n + r * h_n)
+    return (1.0 - z) * n + z * h
+
+
+def compute_advantages(critic, reward, done, gamma, gae_coef=0.0):
+    """base_ac.py:185-198."""
+    tds = (reward + gamma * (1.0 - done) * critic[:, 1:].detach()) - critic[:, :-1]
+    if gae_coef <= 0:
+        return tds
+    gae = torch.zeros_like(tds[:, -1])
+    gaes = []
+    for t in range(tds.shape[1] - 1, -1, -1):
+        gae = tds[:, t] + gamma * gae_coef * (1.0 - done[:, t]) * gae
+        gaes.insert(0, gae)
+    return torch.stack(gaes, dim=1)
+
+
+def a2c_loss(out, actions, reward, done, gamma, entropy_coef, vf_coef, gae_coef=0.0):
+    """base_ac.py:200-217 on a forward output: actions [N, T+1] (entry 0 = the action before the window),
+    reward / done [N, T] (the targets of entries 1..T)."""
+    logits = out['logits'][:, :-1]
+    critic = out['critic']
+    entropy_loss = Categorical(logits=logits).entropy().mean(-1)
+    advantages = compute_advantages(critic, reward, done, gamma, gae_coef)
+    value_loss = advantages.pow(2).mean(-1)
+    log_ap = torch.log_softmax(logits, -1)
+    log_ap = torch.gather(log_ap, dim=-1, index=actions[:, 1:].unsqueeze(-1)).squeeze(-1)
+    a2c = -(advantages.detach() * log_ap).mean(-1)
+    loss = a2c + vf_coef * value_loss - entropy_coef * entropy_loss
+    return loss.mean()
+
+
+class BatchedA2C:
+    """A2C with a shared ``RecurrentAC`` over B envs x A agents of one engine, everything on the device.
+
+    Per step: the engine renders o_t as packed rows + the fused ``obs_proj`` (one kernel, no dense obs); the
+    policy acts on (o_t, a_{t-1}, h_t); actions go straight back into ``mfg_step`` (int32 on the device).
+    Every ``n_steps`` steps: one A2C update on the window o_0..o_T (``base_ac.py:126-128``), with obs_proj
+    re-evaluated by ``embedding_bag`` over the stored entries. No host synchronisation inside ``step``;
+    ``learn`` syncs once when ``check_cap`` is set (truncated packed rows raise)."""
+
+    def __init__(self, factory, net=None, n_steps=5, gamma=0.99, entropy_coef=0.01, vf_coef=0.5, gae_coef=0.0,
+                 lr=3e-4, cap=32, obs_emb_size=96, action_emb_size=16, hidden_size=64, use_agent_embedding=False,
+                 check_cap=True, generator=None):
+        from .engine import PackedObs
+        self.f = factory
+        eng = factory.engine
+        spec = factory.spec
+        self.B, self.A = eng.B, eng.A
+        self.N = self.B * self.A
+        self.dev = eng.device
+        n_act = set(int(x) for x in spec.n_actions)
+        if len(n_act) != 1:
+            raise ValueError('BatchedA2C shares one network: all agents need the same number of actions')
+        self.n_actions = n_act.pop()
+        kdim = eng.lmax * eng.obs_hw[0] * eng.obs_hw[1]
+        self.net = net if net is not None else RecurrentAC(
+            kdim, self.n_actions, obs_emb_size, action_emb_size, hidden_size, hidden_size, self.A,
+            use_agent_embedding=use_agent_embedding)
+        self.net.to(self.dev)
+        self.opt = torch.optim.RMSprop(self.net.parameters(), lr=lr, eps=1e-5)
+        self.T, self.gamma, self.entropy_coef, self.vf_coef, self.gae_coef = n_steps, gamma, entropy_coef, \
+            vf_coef, gae_coef
+        self.check_cap = check_cap
+        self.gen = generator
+        T, N, dev = self.T, self.N, self.dev
+        # obs slots o_0..o_T of the window (entries + fused projection), written by the engine
+        self.pobs = PackedObs(eng, K=T + 1, cap=cap, weight=self.net.obs_proj.weight, bias=self.net.obs_proj.bias)
+        self.slot = [self.pobs.view(k) for k in range(T + 1)]
+        self.act_in = torch.full((T + 1, self.B, self.A), -1, dtype=torch.int64, device=dev)  # a_{t-1}, -1 = none
+        self.act = torch.zeros((T, self.B, self.A), dtype=torch.int32, device=dev)
+        self.rew = torch.zeros((T, self.B, self.A), dtype=torch.float64, device=dev)
+        self.done = torch.zeros((T, self.B), dtype=torch.uint8, device=dev)
+        H = self.net.hidden_size_actor
+        self.h0a = torch.zeros((N, 1, H), device=dev)  # hidden state fed at entry 0 of the window
+        self.h0c = torch.zeros((N, 1, self.net.hidden_size_critic), device=dev)
+        self.ha, self.hc = self.h0a.clone(), self.h0c.clone()
+        self.agent_ids = torch.arange(self.A, device=dev).repeat(self.B)
+        self.t = 0
+        self.updates = 0
+        self.episodes = torch.zeros((), dtype=torch.float64, device=dev)
+        self.reward_sum = torch.zeros((), dtype=torch.float64, device=dev)
+        self._started = False
+
+    def reset(self):
+        self.f.engine.reset(obs=self.slot[0], init=0 if self.f._created else 1, seed_base=self.f.seed_base)
+        self.f._created = True
+        self._started = True
+        self.t = 0
+
+    @torch.no_grad()
+    def step(self):
+        """One env-step of every env with the current policy (no host sync)."""
+        if not self._started:
+            self.reset()
+        t = self.t
+        emb = self.pobs.emb[t].view(self.N, 1, -1)
+        a_in = self.act_in[t].view(self.N, 1)
+        out = self.net.forward_emb(emb, a_in, self.ha, self.hc, agent_ids=self.agent_ids)
+        logits = out['logits'][:, 0]
+        if self.gen is None:
+            a = Categorical(logits=logits).sample()
+        else:
+            a = torch.multinomial(torch.softmax(logits, -1), 1, generator=self.gen).squeeze(-1)
+        self.act[t].copy_(a.view(self.B, self.A))
+        self.f.engine.step(1, actions=self.act[t], reward=self.rew[t], done=self.done[t], obs=self.slot[t + 1],
+                           auto_reset=True, step_base=self.f.t)
+        self.f.t += 1
+        d = self.done[t].bool()
+        # the next entry's inputs: last action (-1 after an episode end) and the recurrent state (zero then)
+        self.act_in[t + 1].copy_(torch.where(d.view(-1, 1), torch.full_like(a.view(self.B, self.A), -1),
+                                             a.view(self.B, self.A)))
+        keep = (~d).repeat_interleave(self.A).view(self.N, 1, 1).to(self.ha.dtype)
+        self.ha = out['hidden_actor'] * keep
+        self.hc = out['hidden_critic'] * keep
+        self.episodes += d.sum()
+        self.reward_sum += self.rew[t].sum()
+        self.t += 1
+        if self.t == self.T:
+            self.learn()
+
+    def window(self):
+        """The window's learner inputs: packed entries [N, T+1, cap], action inputs [N, T+1], starts,
+        targets."""
+        T, N = self.T, self.N
+        idx = self.pobs.idx.permute(1, 2, 0, 3).reshape(N, T + 1, -1)
+        val = self.pobs.val.permute(1, 2, 0, 3).reshape(N, T + 1, -1)
+        a_in = self.act_in.permute(1, 2, 0).reshape(N, T + 1)
+        acts = torch.cat([a_in[:, :1], self.act.permute(1, 2, 0).reshape(N, T).long()], 1)
+        d = self.done.permute(1, 0).repeat_interleave(self.A, 0).to(torch.float32)  # [N, T]
+        starts = torch.cat([torch.zeros((N, 1), dtype=torch.bool, device=self.dev), d.bool()], 1)
+        rew = self.rew.permute(1, 2, 0).reshape(N, T).to(torch.float32)
+        return idx, val, a_in, acts, starts, rew, d
+
+    def learn(self):
+        """One A2C update on the window (base_ac.py:200-225), then slide: o_T becomes o_0."""
+        if self.check_cap:
+            self.pobs.check()
+        idx, val, a_in, acts, starts, rew, d = self.window()
+        with torch.enable_grad():
+            emb = self.net.project_packed(idx, val)
+            out = self.net.forward_emb(emb, a_in, self.h0a, self.h0c, agent_ids=self.agent_ids, starts=starts)
+            loss = a2c_loss(out, acts, rew, d, self.gamma, self.entropy_coef, self.vf_coef, self.gae_coef)
+            self.opt.zero_grad()
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(self.net.parameters(), 0.5)
+            self.opt.step()
+        self.last_loss = loss.detach()
+        self.updates += 1
+        with torch.no_grad():
+            T = self.T
+            self.pobs.idx[0].copy_(self.pobs.idx[T])
+            self.pobs.val[0].copy_(self.pobs.val[T])
+            self.pobs.count[0].copy_(self.pobs.count[T])
+            self.act_in[0].copy_(self.act_in[T])
+            self.h0a, self.h0c = self.ha.clone(), self.hc.clone()
+            # new weights: the engine projects with them from now on; o_0's projection is redone here
+            self.pobs.set_projection(self.net.obs_proj.weight, self.net.obs_proj.bias)
+            self.pobs.emb[0].copy_(self.net.project_packed(self.pobs.idx[0], self.pobs.val[0]))
+        self.t = 0
+
+    def train(self, n_updates):
+        for _ in range(n_updates * self.T):
+            self.step()
+        return self.last_loss

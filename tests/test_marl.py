@@ -1,0 +1,189 @@
+"""On-GPU MARL over packed observations (mfg_amd/marl.py).
+
+CPU: the learner (RecurrentAC fed by packed obs through embedding_bag + the A2C loss) against golden vectors
+produced by the reference's own network and loss (tests/golden/marl_a2c.npz, tools/gen_golden_marl.py:
+algorithms/marl/networks.py RecurrentAC, algorithms/marl/base_ac.py actor_critic/learn). f32 arithmetic in a
+different summation order: loss and gradients within 1e-5 relative (+1e-7 absolute), weights after one
+RMSprop step within 1e-6 absolute.
+GPU: the engine's packed rows scatter back to the dense f32 obs bit-exactly, its fused projection matches a
+torch f64 GEMM of the dense obs within 1e-5 relative, and the A2C loop trains on the device.
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from mfg_amd.marl import RecurrentAC, a2c_loss
+
+GOLD = Path(__file__).resolve().parent / 'golden' / 'marl_a2c.npz'
+
+
+def pack(obs, cap):
+    """Dense [N, T, ...] -> (idx u16, val f32) [N, T, cap] of the nonzero entries of obs.float()."""
+    flat = torch.as_tensor(obs).reshape(obs.shape[0], obs.shape[1], -1).float()
+    N, T, K = flat.shape
+    idx = torch.zeros((N, T, cap), dtype=torch.uint16)
+    val = torch.zeros((N, T, cap), dtype=torch.float32)
+    for n in range(N):
+        for t in range(T):
+            nz = torch.nonzero(flat[n, t]).flatten()
+            assert len(nz) <= cap
+            idx[n, t, :len(nz)] = nz.to(torch.uint16)
+            val[n, t, :len(nz)] = flat[n, t, nz]
+    return idx, val
+
+
+def load_case(z, i):
+    c = {k.split('.', 1)[1]: z[k] for k in z.files if k.startswith(f'c{i}.')}
+    st = {k[2:]: torch.from_numpy(v) for k, v in c.items() if k.startswith('w.')}
+    N, T1 = c['actions'].shape
+    obs_shape = c['obs'].shape[2:]
+    net = RecurrentAC(observation_size=obs_shape, n_actions=int(c['n_actions']),
+                      obs_emb_size=st['obs_proj.weight'].shape[0], action_emb_size=st['action_emb.weight'].shape[1],
+                      hidden_size_actor=st['gru_actor.weight_hh_l0'].shape[1],
+                      hidden_size_critic=st['gru_critic.weight_hh_l0'].shape[1], n_agents=N,
+                      use_agent_embedding=bool(c['use_agent_embedding']))
+    net.load_state_dict(st)
+    return c, net
+
+
+@pytest.mark.parametrize('i', [0, 1, 2])
+def test_a2c_learner_matches_reference(i):
+    z = np.load(GOLD)
+    c, net = load_case(z, i)
+    N = c['actions'].shape[0]
+    idx, val = pack(c['obs'], cap=64)
+    acts = torch.from_numpy(c['actions']).long()
+    emb = net.project_packed(idx, val)
+    out = net.forward_emb(emb, acts, torch.from_numpy(c['ha0']), torch.from_numpy(c['hc0']),
+                          agent_ids=torch.arange(N))
+    loss = a2c_loss(out, acts, torch.from_numpy(c['reward'])[:, 1:], torch.from_numpy(c['done'])[:, 1:],
+                    gamma=0.99, entropy_coef=0.01, vf_coef=0.5, gae_coef=float(c['gae_coef']))
+    ref = float(c['loss'])
+    assert abs(loss.item() - ref) <= 1e-5 * abs(ref) + 1e-7, (loss.item(), ref)
+    opt = torch.optim.RMSprop(net.parameters(), lr=3e-4, eps=1e-5)
+    opt.zero_grad()
+    loss.backward()
+    for k, p in net.named_parameters():
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        gr = torch.from_numpy(c['g.' + k])
+        assert torch.allclose(g, gr, rtol=1e-4, atol=1e-6), (k, (g - gr).abs().max())
+    torch.nn.utils.clip_grad_norm_(net.parameters(), 0.5)
+    opt.step()
+    for k, p in net.named_parameters():
+        assert torch.allclose(p.detach(), torch.from_numpy(c['a.' + k]), rtol=0, atol=1e-6), k
+
+
+def test_dense_forward_is_the_reference_forward():
+    """The reference-signature forward (dense obs) equals the packed path on the same inputs."""
+    z = np.load(GOLD)
+    c, net = load_case(z, 0)
+    acts = torch.from_numpy(c['actions']).long()
+    ha, hc = torch.from_numpy(c['ha0']), torch.from_numpy(c['hc0'])
+    dense = net(torch.from_numpy(c['obs']), acts, ha, hc)
+    idx, val = pack(c['obs'], cap=64)
+    packed = net.forward_emb(net.project_packed(idx, val), acts, ha, hc)
+    for k in ('logits', 'critic'):
+        assert torch.allclose(dense[k], packed[k], rtol=1e-5, atol=1e-6), k
+
+
+def test_stepwise_restarts():
+    """starts=all-False equals one GRU call; a start at entry s equals a fresh run from s with zero state."""
+    torch.manual_seed(0)
+    net = RecurrentAC((3, 4, 4), 5, 16, 4, 8, 8, 3, use_agent_embedding=False)
+    N, T = 3, 6
+    emb = torch.randn(N, T, 16)
+    acts = torch.randint(-1, 5, (N, T))
+    h = torch.randn(N, 1, 8)
+    full = net.forward_emb(emb, acts, h, h)
+    st = net.forward_emb(emb, acts, h, h, starts=torch.zeros(N, T, dtype=torch.bool))
+    assert torch.allclose(full['logits'], st['logits'], atol=1e-6)
+    starts = torch.zeros(N, T, dtype=torch.bool)
+    starts[:, 3] = True
+    r = net.forward_emb(emb, acts, h, h, starts=starts)
+    fresh = net.forward_emb(emb[:, 3:], acts[:, 3:], torch.zeros_like(h), torch.zeros_like(h))
+    assert torch.allclose(r['logits'][:, 3:], fresh['logits'], atol=1e-6)
+    assert torch.allclose(r['critic'][:, :3], full['critic'][:, :3], atol=1e-6)
+
+
+# ---------------------------------------------------------------------------------------------------------
+# GPU: the engine's packed mode
+# ---------------------------------------------------------------------------------------------------------
+def _engine_pair(cfg, B, K, E=96, cap=64, seed_base=0):
+    from mfg_amd.spec import compile_spec
+    from mfg_amd.engine import Engine, PackedObs
+    spec = compile_spec(cfg)
+    dense, packed = Engine(spec, B, device=0), Engine(spec, B, device=0)
+    kdim = dense.lmax * dense.obs_hw[0] * dense.obs_hw[1]
+    g = torch.Generator().manual_seed(1)
+    w = (torch.randn(E, kdim, generator=g) * 0.1).cuda()
+    b = (torch.randn(E, generator=g) * 0.1).cuda()
+    po = PackedObs(packed, K=K, cap=cap, weight=w, bias=b)
+    return spec, dense, packed, po, w, b
+
+
+def _check_rows(dense_obs, po, w, b, k):
+    """Packed row k == dense f32 obs bit-exactly; emb == f64 GEMM within 1e-5 relative."""
+    B, A = dense_obs.shape[:2]
+    flat = dense_obs.reshape(B, A, -1)
+    nnz = (flat != 0).sum(-1).to(torch.int32)
+    assert torch.equal(po.count[k], nnz)
+    assert torch.equal(po.dense(k).reshape(B, A, -1), flat)
+    ref = flat.double() @ w.double().t() + b.double()
+    err = (po.emb[k].double() - ref).abs()
+    tol = 1e-5 * (flat.double().abs() @ w.double().abs().t() + b.double().abs()) + 1e-6
+    assert bool((err <= tol).all()), float(err.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('cfg,B,K', [('large8.yaml', 2048, 8), ('rooms4.yaml', 512, 4), ('alltest16.yaml', 96, 2),
+                                     ('simple1.yaml', 256, 4)])
+def test_packed_obs_matches_dense(cfg, B, K):
+    spec, dense, packed, po, w, b = _engine_pair(cfg, B, K)
+    obs = torch.zeros(dense.obs_shape(K), dtype=torch.float32, device='cuda')
+    dense.reset(obs=obs[0], init=True, seed_base=5)
+    packed.reset(obs=po.view(0), init=True, seed_base=5)
+    _check_rows(obs[0], po, w, b, 0)
+    for it in range(3):
+        dense.step(K, philox_seed=9, step_base=1 + it * K, obs=obs, auto_reset=True)
+        packed.step(K, philox_seed=9, step_base=1 + it * K, obs=po, auto_reset=True)
+        for k in range(K):
+            _check_rows(obs[k], po, w, b, k)
+    dense.close()
+    packed.close()
+
+
+@pytest.mark.gpu
+def test_packed_cap_truncation_is_reported():
+    spec, dense, packed, po, w, b = _engine_pair('large8.yaml', 256, 1, cap=2)
+    obs = torch.zeros(dense.obs_shape(1), dtype=torch.float32, device='cuda')
+    dense.reset(obs=obs[0], init=True)
+    packed.reset(obs=po, init=True)
+    flat = obs[0].reshape(256, spec.n_agents, -1)
+    assert torch.equal(po.count[0], (flat != 0).sum(-1).to(torch.int32))
+    # the projection covers all entries even when the stored row is truncated
+    ref = flat.double() @ w.double().t() + b.double()
+    assert float((po.emb[0].double() - ref).abs().max()) < 1e-3
+    with pytest.raises(RuntimeError):
+        po.check()
+
+
+@pytest.mark.gpu
+def test_batched_a2c_trains_on_device():
+    from mfg_amd.factory import BatchedFactory
+    from mfg_amd.marl import BatchedA2C
+    f = BatchedFactory('large8.yaml', 512, seed_base=3)
+    tr = BatchedA2C(f, n_steps=5, generator=torch.Generator(device='cuda').manual_seed(0))
+    w0 = tr.net.obs_proj.weight.detach().clone()
+    loss = tr.train(4)
+    assert tr.updates == 4 and torch.isfinite(loss)
+    assert not torch.equal(w0, tr.net.obs_proj.weight.detach())
+    # after the updates the engine projects with the new weights: emb of o_0 == embedding_bag of its entries
+    e = tr.net.project_packed(tr.pobs.idx[0], tr.pobs.val[0])
+    assert torch.allclose(e, tr.pobs.emb[0], rtol=1e-5, atol=1e-5)
+    # one more step renders with the refreshed weights inside the kernel
+    tr.step()
+    e1 = tr.net.project_packed(tr.pobs.idx[1], tr.pobs.val[1])
+    assert torch.allclose(e1, tr.pobs.emb[1], rtol=1e-5, atol=1e-5)
+    f.close()

@@ -66,7 +66,7 @@ def test_hip_library_exports_every_declared_symbol():
     for f in funcs:
         assert hasattr(lib, f), f'{f} declared in include/mfg.h but not exported'
     lib.mfg_abi_version.restype = C.c_int
-    assert lib.mfg_abi_version() == 2
+    assert lib.mfg_abi_version() == 3
 
 
 def _hip_lib():
@@ -161,6 +161,8 @@ def test_struct_layouts_agree():
     assert C.sizeof(abi.MfgSpec) == L.oracle_sizeof_spec()
     assert C.sizeof(abi.MfgEvents) == L.oracle_sizeof_events()
     assert C.sizeof(O.Res) == L.oracle_sizeof_res()
+    L.oracle_sizeof_packed_obs.restype = C.c_int
+    assert C.sizeof(abi.MfgPackedObs) == L.oracle_sizeof_packed_obs()
 
 
 def test_philox_known_answer():
