@@ -20,6 +20,7 @@ import numpy as np
 
 from . import abi
 from .engine import Engine, PackedObs, RecordView, events_from_rows, EV_MISC, HDR, HDR_N
+from .host_rules import HostRules, StateView, fold_step, level_map, pre_snapshot
 from .info import rebuild_info
 from .spec import compile_spec, UnsupportedSpec
 from . import views as _views
@@ -66,12 +67,13 @@ class Factory:
 
     def __init__(self, config_file, custom_modules_path=None, custom_level_path=None, *, device=0,
                  sync_python_random=True, py_seed=None):
-        if custom_modules_path is not None:
-            raise UnsupportedSpec('custom_modules_path: user plugin classes cannot run in the HIP engine')
         import torch
         self._torch = torch
         self._config_file = config_file
-        self.spec = compile_spec(config_file, custom_level_path)
+        # custom Rule classes from custom_modules_path run on the host beside the engine (mfg_amd/host_rules.py)
+        self.spec = compile_spec(config_file, custom_level_path, custom_modules_path)
+        self._host = HostRules(self.spec) if self.spec.host_rules else None
+        self._host_init = False
         self._eng = Engine(self.spec, 1, device=device)
         self._dev = self._eng.device
         self._sync = sync_python_random and py_seed is None
@@ -156,6 +158,12 @@ class Factory:
         self._torch.cuda.synchronize(self._dev)
         self._agent_states = None
         self._step = 0
+        if self._host:
+            view = StateView(self.spec, self.snapshot())
+            if not self._host_init:  # rules.do_all_init (factory.py:121); the view is the reset state here
+                self._host.on_init(view, level_map(self.spec))
+                self._host_init = True
+            self._host.on_reset(view)
         return {f'Agent[{n}]': o for n, o in zip(self.spec.agent_names, self._obs_list())}
 
     def step(self, actions):
@@ -169,6 +177,9 @@ class Factory:
             if not 0 <= int(x) < self.spec.n_actions[a]:
                 raise IndexError(f'action {x} out of range for agent {a}')
         self._act.copy_(self._torch.tensor([actions], dtype=self._torch.int32))
+        pre = None
+        if self._host:  # the state the host rules' tick_pre_step sees: before the actions (states.py:181-187)
+            pre = pre_snapshot(self.snapshot())
         if self._sync:
             self._push_random()
         self._eng.step(1, actions=self._act, reward=self._rew, done=self._done, obs=self._obs, ev_act=self._ev_a,
@@ -180,10 +191,15 @@ class Factory:
         if ev['crashed']:
             raise RuntimeError('the reference crashes on this step (SURVEY App. A Q9/Q17); env state is flagged')
         reward = [float(x) for x in self._rew[0].cpu().numpy()]
-        info = dict(rebuild_info(self.spec, [int(x) for x in actions], ev, reward))
         done = bool(self._done.item())
         self._step = ev['step']
         self._agent_states = _views.agent_states(self.spec, actions, ev_a, ev_w)
+        if self._host:  # custom rules: their Results join the device's in rule order, then one fold
+            reward, done, info = fold_step(self.spec, self._host, [int(x) for x in actions], ev, pre,
+                                           self.snapshot(), done)
+            info = dict(info)
+        else:
+            info = dict(rebuild_info(self.spec, [int(x) for x in actions], ev, reward))
         self._last = (reward, done, info)
         return None, self._obs_list(), reward, done, info
 

@@ -252,7 +252,7 @@ def _parse_actions(conf_actions):
     return out
 
 
-def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpec:
+def compile_spec(config_path, custom_level_path: Optional[str] = None, custom_modules_path: Optional[str] = None) -> EnvSpec:
     config_path = Path(config_path)
     if not config_path.exists() and (CONFIGS_DIR / config_path.name).exists():
         config_path = CONFIGS_DIR / config_path.name
@@ -383,12 +383,22 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
     if 'Defaults' in rules_conf:
         raise UnsupportedSpec("Rules: Defaults loads 'WatchCollision' and exits upstream (Q23)")
     rules, rule_names = [], []
+    host_rules = []  # custom rules (custom_modules_path) run on the host: (slot, name, class, kwargs)
     battery_cost_dict = None
     dest_entries = []
     for rname, rkw in rules_conf.items():
         rkw = rkw or {}
         if rname not in _RULES:
-            raise UnsupportedSpec(f'rule {rname!r} is not implemented by the engine')
+            # config_parser.py:218-233: built-in folders first, then the custom path
+            cls = None
+            if custom_modules_path is not None:
+                from .host_rules import locate_custom_class
+                cls = locate_custom_class(rname, custom_modules_path)
+            if cls is None:
+                raise UnsupportedSpec(f'rule {rname!r} is not implemented by the engine'
+                                      + (f' and not found in {custom_modules_path}' if custom_modules_path else ''))
+            host_rules.append((len(rules), rname, cls, rkw))
+            continue
         op = _RULES[rname]
         ri, rf = [0] * 6, [0.0] * 6
         if op == abi.RULE_DOOR_AUTOCLOSE:
@@ -519,6 +529,7 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None) -> EnvSpe
     es.agent_positions = agent_positions
     es.battery_cost_dict = battery_cost_dict
     es.dest_entries = dest_entries
+    es.host_rules = host_rules
     es.c = _to_c(es)
     return es
 

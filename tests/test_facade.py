@@ -29,11 +29,13 @@ def test_compat_import_path():
         sys.path.remove(str(COMPAT))
 
 
-def test_custom_modules_rejected():
+def test_custom_rule_missing_from_custom_path_rejected():
+    """A rule found neither built in nor under custom_modules_path is a clean UnsupportedSpec (the reference
+    exits, config_parser.py:238-249); found ones run on the host (tests/test_host_rules.py)."""
     from mfg_amd.factory import Factory
     from mfg_amd.spec import UnsupportedSpec
     with pytest.raises(UnsupportedSpec):
-        Factory('large8.yaml', custom_modules_path='/tmp/nowhere')
+        Factory('custom_rules4.yaml', custom_modules_path='/tmp/nowhere')
 
 
 def test_no_cpu_fallback():

@@ -1,0 +1,111 @@
+"""Custom-plugin fallback (mfg_amd/host_rules.py): user Rule classes from custom_modules_path
+(tests/custom_rules/rules.py) run on the host beside the engine; their Results merge into the step's Result
+list in rule order. Pinned by reference fixtures (tests/golden/custom_rules4_s*.json.gz, tools/gen_golden_custom.py):
+rewards bit-exact (f64 ==), done and the info dict equal, every step, across episode ends.
+
+The reference's own loader exits on any custom rule (config_parser.py:238 tests `(e1 and e2) or e3`, so a class
+missing from both built-in folders aborts even after the custom path found it); the fixtures record the reference
+with that lookup succeeding (see tools/gen_golden_custom.py).
+CPU: the C oracle (test infrastructure) provides the device part; GPU: the engine through mfg_amd.Factory.
+"""
+import gzip
+import json
+import random
+import sys
+from pathlib import Path
+
+import pytest
+
+import golden_compare as G
+
+ROOT = Path(__file__).resolve().parent.parent
+CUSTOM = ROOT / 'tests' / 'custom_rules'
+COMPAT = ROOT / 'marl-factory-grid_amd' / 'compat'
+CFG = 'custom_rules4.yaml'
+
+
+@pytest.fixture
+def compat_path(monkeypatch):
+    monkeypatch.syspath_prepend(str(COMPAT))
+    for m in [m for m in sys.modules if m.startswith('marl_factory_grid') or m.startswith('mfg_custom_')]:
+        monkeypatch.delitem(sys.modules, m)
+
+
+def _load(seed):
+    with gzip.open(ROOT / 'tests' / 'golden' / f'custom_rules4_s{seed}.json.gz', 'rt') as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize('seed', [0, 1])
+def test_host_rules_match_reference_on_oracle(seed, compat_path):
+    import oracle as O
+    from views_compare import oracle_snapshot
+    from mfg_amd.spec import compile_spec
+    from mfg_amd.host_rules import HostRules, StateView, fold_step, level_map, pre_snapshot
+    rec = _load(seed)
+    spec = compile_spec(CFG, custom_modules_path=str(CUSTOM))
+    assert [n for _, n, _, _ in spec.host_rules] == ['PenaltyBeforeActions', 'CountFailedActions',
+                                                      'DoorProximityBonus', 'DoneWhenCrowded']
+    env = O.OracleEnv(spec, rec['py_seed'])
+    env.reset()
+    host = HostRules(spec)
+    host.on_init(StateView(spec, oracle_snapshot(env)), level_map(spec))
+    host.on_reset(StateView(spec, oracle_snapshot(env)))
+    n_done = 0
+    for r in rec['steps']:
+        pre = pre_snapshot(oracle_snapshot(env))
+        _, ddone, ev = env.step(r['actions'], with_obs=False)
+        reward, done, info = fold_step(spec, host, r['actions'], ev, pre, oracle_snapshot(env), ddone)
+        assert reward == r['reward'], (r['t'], reward, r['reward'])
+        assert done == r['done'], r['t']
+        ok, bad = G.info_equal(info, r['info'])
+        assert ok, (r['t'], bad)
+        if done:
+            n_done += 1
+            env.reset()
+            host.on_reset(StateView(spec, oracle_snapshot(env)))
+    assert n_done >= 3  # crowding and max-steps ends are both exercised
+    env.close()
+
+
+def test_custom_rules_need_the_custom_path(compat_path):
+    from mfg_amd.spec import compile_spec, UnsupportedSpec
+    with pytest.raises(UnsupportedSpec):
+        compile_spec(CFG)
+
+
+def test_host_view_is_read_only(compat_path):
+    import oracle as O
+    from views_compare import oracle_snapshot
+    from mfg_amd.spec import compile_spec
+    from mfg_amd.host_rules import StateView
+    spec = compile_spec(CFG, custom_modules_path=str(CUSTOM))
+    env = O.OracleEnv(spec, 0)
+    env.reset()
+    view = StateView(spec, oracle_snapshot(env))
+    agent = view['Agent'][0]
+    with pytest.raises(AttributeError):
+        agent.pos = (1, 1)
+    assert len(view['Doors']) == spec.c.n_doors and view.curr_step == 0
+    assert agent in view.entities.pos_dict[agent.pos]
+    env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('seed', [0, 1])
+def test_factory_with_custom_rules_matches_reference(seed, compat_path):
+    from mfg_amd.factory import Factory
+    rec = _load(seed)
+    random.seed(rec['py_seed'])
+    env = Factory(str(ROOT / 'marl-factory-grid_amd' / 'mfg_amd' / 'configs' / CFG),
+                  custom_modules_path=str(CUSTOM))
+    env.reset()
+    for r in rec['steps']:
+        _, _, reward, done, info = env.step(r['actions'])
+        assert reward == r['reward'], r['t']
+        assert done == r['done'], r['t']
+        ok, bad = G.info_equal(info, r['info'])
+        assert ok, (r['t'], bad)
+        if done:
+            env.reset()
+    env.close() if hasattr(env, 'close') else None

@@ -53,7 +53,7 @@ def test_ray_table_matches_reference(r):
 def test_oracle_replays_reference_fixture(tag, cfg, seed):
     import oracle as O
     from mfg_amd.spec import compile_spec
-    from mfg_amd.info import rebuild_info
+    from mfg_amd.info import rebuild_info, rebuild_rewards, step_results
     rec, npz = G.load(tag, seed)
     spec = compile_spec(cfg)
     env = O.OracleEnv(spec, rec['py_seed'])
@@ -71,6 +71,9 @@ def test_oracle_replays_reference_fixture(tag, cfg, seed):
                 continue
             if [float(x) for x in rew] != r['reward']:
                 errs.append((t, 'reward'))
+            # the host replay of the Result list (custom host rules merge into it) folds to the same f64 rewards
+            if rebuild_rewards(spec, step_results(spec, r['actions'], ev)) != r['reward']:
+                errs.append((t, 'host reward fold'))
             if done != r['done']:
                 errs.append((t, 'done'))
             ok, bad = G.info_equal(rebuild_info(spec, r['actions'], ev, list(rew)), r['info'])
