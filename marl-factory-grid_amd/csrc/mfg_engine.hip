@@ -1082,6 +1082,143 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
   if (e.lane == a) o.my_act_ev = 0x80 | (valid ? 1 : 0) | (coll ? 2 : 0) | (aux ? 4 : 0);
 }
 
+// Agents act in list order (states.py:189-198), but most actions only depend on the agents before them
+// through positions and door states: Noop, Move (no blocking agents in the spec), Charge, DoorUse, and an
+// ItemAction on a cell without items or drop-offs (it fails). The leading run 0..F-1 of such agents is
+// resolved lane-parallel (lane = agent); the ordered loop continues from the first other one (F):
+//   * door state seen by agent a = initial state XOR the parity of the toggles of DoorUse agents b < a;
+//   * cell occupancy seen by agent a = agents b < a at their new cells + agents b > a at their old ones;
+//   * arrival order = the running counter + the exclusive count of earlier successful movers;
+//   * floor-shuffle debt (Q3) = one per unblocked target + one per successful move, summed.
+// Each agent's own reward terms keep their order (the action result is its first term).
+__device__ int act_parallel(const Env& e, int my_act, StepOut& o) {
+  SpecP S = e.S;
+  const int A = S->A, W = S->s.W, lane = e.lane;
+  const bool me = lane < A;
+  const int al = me ? lane : 0;
+  const bool par = me && e.agpar()[al] != 0;
+  const bool ok_slot = me && my_act >= 0 && my_act < S->s.n_actions[al];
+  const CS mfg_action& ac = S->s.actions[al][ok_slot ? my_act : 0];
+  const int op = ok_slot ? ac.op : -1;
+  const int pos = me ? e.agpos()[al] : -1;
+  const bool any_blocking = ballot(me && S->s.agent_blocking[al]) != 0;
+  bool simple = !me || par;
+  if (me && !par && ok_slot) {
+    if (op == MFG_ACT_NOOP || op == MFG_ACT_CHARGE || op == MFG_ACT_DOORUSE) simple = true;
+    else if (op == MFG_ACT_MOVE) simple = !any_blocking;
+    else if (op == MFG_ACT_ITEM) {
+      bool hit = false;
+      const int ni = e.H(H_N_ITEMS), ndr = e.H(H_N_DROPS);
+      for (int i = 0; i < ni; i++) { const int w = e.items()[i]; hit |= EW_POS(w) == pos && (w & EW_ALIVE); }
+      for (int i = 0; i < ndr; i++) { const int w = e.drops()[i]; hit |= EW_POS(w) == pos && (w & EW_ALIVE); }
+      simple = !hit;
+    }
+  }
+  const u64 ns = ballot(!simple);
+  const int F = ns ? ffs64(ns) : A;
+  if (F == 0) return 0;
+  const bool act = me && lane < F && !par;
+  // DoorUse: the present doors in the 3x3 around the agent (doors/actions.py:18-34)
+  const int x = pos >= 0 ? pos / W : 0, y = pos >= 0 ? pos - x * W : 0;
+  u64 tm = 0;
+  if (act && op == MFG_ACT_DOORUSE) {
+    for (int k = 0; k < 9; k++) {
+      const int px = x + k / 3 - 1, py = y + k % 3 - 1;
+      if (px < 0 || py < 0 || px >= S->s.H || py >= W) continue;
+      const int c = px * W + py;
+      if (S->level[c] == 1) continue;
+      const int d = S->door_of[c];
+      if (d != 0xFF && (e.door()[d] & DW_PRESENT)) tm |= 1ull << d;
+    }
+  }
+  const u64 tm_lanes = ballot(tm != 0);
+  u64 seen = 0;  // doors toggled by DoorUse agents before this one
+  for (u64 m = tm_lanes; m; m &= m - 1) {
+    const int b = ffs64(m);
+    const u64 tb = ((u64)(uint32_t)rl((int)(uint32_t)(tm >> 32), b) << 32) | (uint32_t)rl((int)(uint32_t)tm, b);
+    if (b < lane) seen ^= tb;
+  }
+  // Move: target, blocking as this agent sees it (walls, closed present doors; states.py:240-270)
+  static const int DX[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
+  static const int DY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+  const bool mv = act && op == MFG_ACT_MOVE;
+  const int t = mv ? pos + DX[ac.arg] * W + DY[ac.arg] : 0;  // levels are wall-bounded
+  bool blocked = false;
+  if (mv) {
+    blocked = S->level[t] == 1;
+    const int d = S->door_of[t];
+    if (!blocked && d != 0xFF) {
+      const int w = e.door()[d];
+      const bool open = ((w & DW_OPEN) != 0) ^ (((seen >> d) & 1) != 0);
+      blocked = (w & DW_PRESENT) && !open;
+    }
+  }
+  const bool vmove = mv && !blocked && t != pos;
+  const int npos = vmove ? t : pos;
+  // occupancy seen by this agent at X (its target, or its own cell for Charge)
+  const int X = mv ? t : pos;
+  int cnt = 0;
+  for (int b = 0; b < A; b++) {
+    const int nb = rl(npos, b), ob = rl(pos, b);
+    cnt += (b < lane) ? (nb == X) : ((b > lane) ? (ob == X) : 0);
+  }
+  int mcnt = 0;  // maintainers collide with a mover (colliders_at); Charge counts agents only
+  const int nk = S->kmax ? e.H(H_N_MAINTS) : 0;
+  for (int k = 0; k < nk; k++) { const int w = e.maints()[k]; mcnt += (EW_POS(w) == X && (w & EW_PRESENT)) ? 1 : 0; }
+  int valid = 0, coll = 0;
+  if (act) {
+    if (op == MFG_ACT_NOOP) valid = 1;
+    else if (op == MFG_ACT_MOVE) { valid = vmove; coll = vmove ? cnt + mcnt > 0 : 1; }
+    else if (op == MFG_ACT_DOORUSE) valid = tm != 0;
+    else if (op == MFG_ACT_CHARGE) {  // batteries/actions.py:20-31, entitites.py:98-111
+      bool pod = false;
+      const int np = e.H(H_N_PODS);
+      for (int i = 0; i < np; i++) { const int w = e.pods()[i]; pod |= EW_POS(w) == pos && (w & EW_ALIVE); }
+      const double ch = e.bat()[al];
+      if (pod && ch < 1.0 && cnt == 0) {
+        const double nv = S->s.pod_charge_rate + ch;
+        e.bat()[al] = nv > 1.0 ? 1.0 : nv;
+        valid = 1;
+      }
+    }  // ItemAction here: no item, no drop-off on the cell -> fails
+  }
+  // commit: positions + arrival order, doors, debt, rewards and events
+  const u64 vm = ballot(vmove);
+  const int arr0 = e.H(H_ARRIVAL);
+  const int debt = popc(ballot(mv && !blocked)) + popc(vm);
+  wave_sync();
+  if (vmove) {
+    e.agpos()[al] = t;
+    e.agarr()[al] = arr0 + mbcnt(vm);
+  }
+  if (tm_lanes && lane < S->nd) {  // each door: the parity of its toggles; opening resets the timer
+    int n = 0;
+    for (u64 m = tm_lanes; m; m &= m - 1) {
+      const int b = ffs64(m);
+      const uint32_t lo = (uint32_t)rl((int)(uint32_t)tm, b), hi = (uint32_t)rl((int)(uint32_t)(tm >> 32), b);
+      n += ((lane < 32 ? lo : hi) >> (lane & 31)) & 1;
+    }
+    if (n) {
+      const int w = e.door()[lane];
+      const bool open0 = (w & DW_OPEN) != 0;
+      const bool opened = open0 ? n >= 2 : true;
+      const bool open = open0 ^ ((n & 1) != 0);
+      e.door()[lane] = (w & DW_PRESENT) | (open ? DW_OPEN : 0) | ((opened ? (S->s.door_auto_close & 0xFF) : DW_TTC(w)) << 8);
+    }
+  }
+  if (lane == 0) {
+    e.hdr()[H_ARRIVAL] = arr0 + popc(vm);
+    e.hdr()[H_DEBT] += debt;
+  }
+  if (act) {
+    o.my_rew += valid ? ac.valid_reward : ac.fail_reward;
+    o.my_act_ev = 0x80 | (valid ? 1 : 0) | (coll ? 2 : 0);
+    o.my_slot = my_act;
+  }
+  wave_sync();
+  return F;
+}
+
 // ------------------------------------------------------------------------------------------------
 // rules (environment/rules.py, modules/*/rules.py); hook order states.py:170-226
 // ------------------------------------------------------------------------------------------------
@@ -2376,7 +2513,12 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   e.setH(H_TOTAL_STEPS, e.H(H_TOTAL_STEPS) + 1);
   o.crashed = e.H(H_CRASHED);  // a crash the reset hit (or a crashed env stepped without a reset): done, no step
   wave_sync();
-  for (int a = 0; a < A && !o.crashed; a++) {
+#ifdef MFG_NO_PARLOGIC
+  const int a0 = 0;
+#else
+  const int a0 = o.crashed ? A : act_parallel(e, my_act, o);
+#endif
+  for (int a = a0; a < A && !o.crashed; a++) {
     if (uni(e.agpar()[a])) continue;  // paralyzed agents skip their action
     const int slot = rl(my_act, a);
     if (slot < 0 || slot >= S->s.n_actions[a]) { o.crashed = MFG_CRASH_ACTION; break; }  // IndexError upstream
@@ -2541,7 +2683,18 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
   }
   uint8_t* rec = state + (size_t)env * S->L.size;
   const int bytes = full ? S->L.size : S->L.o_mt;
-  rec_copy(e.lds, rec, bytes, e.lane);
+  // lean records of <= 1 KiB: each lane keeps its 16-B chunk and writes it back only if the step changed it
+  // (most of the record is per-episode constant: frozen origins, ids, counters of idle rules)
+  const bool one_pass = !full && (bytes >> 4) <= MFG_WAVE;
+  uint4 orig = make_uint4(0, 0, 0, 0);
+  if (one_pass) {
+    if (e.lane < (bytes >> 4)) {
+      orig = ((const uint4*)rec)[e.lane];
+      ((uint4*)e.lds)[e.lane] = orig;
+    }
+  } else {
+    rec_copy(e.lds, rec, bytes, e.lane);
+  }
   wave_sync();
   const int A = S->A;
   int my_act = 0;
@@ -2558,7 +2711,14 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
   if (o.done && auto_reset) e.setH(H_DONE, 1);
   wave_sync();
-  rec_copy(rec, e.lds, bytes, e.lane);
+  if (one_pass) {
+    if (e.lane < (bytes >> 4)) {
+      const uint4 v = ((const uint4*)e.lds)[e.lane];
+      if (v.x != orig.x || v.y != orig.y || v.z != orig.z || v.w != orig.w) ((uint4*)rec)[e.lane] = v;
+    }
+  } else {
+    rec_copy(rec, e.lds, bytes, e.lane);
+  }
 }
 
 // Auto-reset of the envs k_logic flagged (H_DONE): pays the shuffle debt, then Factory.reset().

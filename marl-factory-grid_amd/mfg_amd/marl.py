@@ -80,8 +80,7 @@ class RecurrentAC(nn.Module):
         """obs_proj(obs.float()) from packed rows: idx u16 / val f32 [..., cap] -> [..., obs_emb_size]."""
         lead = idx.shape[:-1]
         cap = idx.shape[-1]
-        out = F.embedding_bag(idx.reshape(-1, cap).long(), self.obs_proj.weight.t(),
-                              per_sample_weights=val.reshape(-1, cap), mode='sum')
+        out = _PackedProj.apply(idx.reshape(-1, cap).long(), val.reshape(-1, cap), self.obs_proj.weight.t())
         return (out + self.obs_proj.bias).reshape(*lead, -1)
 
     def forward_emb(self, obs_emb, actions, hidden_actor, hidden_critic, agent_ids=None, starts=None):
@@ -118,6 +117,29 @@ class RecurrentAC(nn.Module):
         return dict(logits=logits, critic=critic, hidden_actor=out_p, hidden_critic=out_c)
 
 
+class _PackedProj(torch.autograd.Function):
+    """x @ W^T over packed rows: forward is a gather-sum of W^T rows (embedding_bag); the weight gradient is
+    D^T @ G with D the rows scattered back to dense, one GEMM (embedding_bag's own backward scatters
+    M x cap x E atomics onto the K x E table, ~100x slower at M = 393K rows)."""
+
+    @staticmethod
+    def forward(ctx, idx, val, wt):
+        ctx.save_for_backward(idx, val)
+        ctx.k = wt.shape[0]
+        return F.embedding_bag(idx, wt, per_sample_weights=val, mode='sum')
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, val = ctx.saved_tensors
+        gw = torch.zeros((ctx.k, g.shape[1]), dtype=g.dtype, device=g.device)
+        step = max(1, (1 << 27) // max(ctx.k, 1))  # dense row blocks of <= 512 MiB
+        for r0 in range(0, idx.shape[0], step):
+            d = torch.zeros((min(step, idx.shape[0] - r0), ctx.k), dtype=g.dtype, device=g.device)
+            d.scatter_add_(1, idx[r0:r0 + step], val[r0:r0 + step].to(g.dtype))
+            gw.addmm_(d.t(), g[r0:r0 + step])
+        return None, None, gw
+
+
 def _gru_cell(gi, h, gru):
     """One nn.GRU step (layer 0) from precomputed input gates gi = x W_ih^T + b_ih."""
     gh = F.linear(h, gru.weight_hh_l0, gru.bias_hh_l0)
@@ -147,7 +169,7 @@ def a2c_loss(out, actions, reward, done, gamma, entropy_coef, vf_coef, gae_coef=
     reward / done [N, T] (the targets of entries 1..T)."""
     logits = out['logits'][:, :-1]
     critic = out['critic']
-    entropy_loss = Categorical(logits=logits).entropy().mean(-1)
+    entropy_loss = Categorical(logits=logits, validate_args=False).entropy().mean(-1)
     advantages = compute_advantages(critic, reward, done, gamma, gae_coef)
     value_loss = advantages.pow(2).mean(-1)
     log_ap = torch.log_softmax(logits, -1)
@@ -226,7 +248,7 @@ class BatchedA2C:
         out = self.net.forward_emb(emb, a_in, self.ha, self.hc, agent_ids=self.agent_ids)
         logits = out['logits'][:, 0]
         if self.gen is None:
-            a = Categorical(logits=logits).sample()
+            a = Categorical(logits=logits, validate_args=False).sample()
         else:
             a = torch.multinomial(torch.softmax(logits, -1), 1, generator=self.gen).squeeze(-1)
         self.act[t].copy_(a.view(self.B, self.A))
