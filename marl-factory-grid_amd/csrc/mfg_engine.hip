@@ -3587,6 +3587,9 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     if (err != hipSuccess) return fail(std::string("k_logic launch: ") + hipGetErrorString(err));
     PROF_END(e, st, MFG_K_LOGIC);
     }
+    // measurement switch: pay the debt every step (before the resets) instead of once per call
+    static const int replay_each = [] { const char* v = getenv("MFG_REPLAY_EACH_STEP"); return v ? atoi(v) : 0; }();
+    if (replay_each && k + 1 < K && replay_impl(e, stream)) return -1;
     if (auto_reset) {
       PROF_BEGIN(e, st);
       hipLaunchKernelGGL(k_resetdone, GEOM(e->h.lds_full), st,

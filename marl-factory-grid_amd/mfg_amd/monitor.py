@@ -137,6 +137,8 @@ class BatchedEpisodeLog:
         if '_final' not in infos:
             return 0
         idx = infos['_final'].nonzero().flatten()
+        if idx.numel() == 0:
+            return 0
         self.returns.append(infos['final_return'][idx].cpu())
         self.lengths.append(infos['final_length'][idx].cpu())
         self.env_ids.append(idx.cpu())

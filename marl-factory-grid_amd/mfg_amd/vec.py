@@ -79,13 +79,13 @@ class VectorFactory:
         term = done_b & ~trunc
         self._ret += rew
         self._len += 1
-        infos = {'done_mask': dm}
-        if bool(done_b.any()):
-            infos['final_return'] = self.torch.where(done_b.unsqueeze(1), self._ret, self.torch.zeros_like(self._ret))
-            infos['final_length'] = self.torch.where(done_b, self._len, self.torch.zeros_like(self._len))
-            infos['_final'] = done_b.clone()
-            self._ret.masked_fill_(done_b.unsqueeze(1), 0.0)
-            self._len.masked_fill_(done_b, 0)
+        # every step carries the final-episode columns (zero where not done): no device->host sync per step
+        infos = {'done_mask': dm,
+                 'final_return': self.torch.where(done_b.unsqueeze(1), self._ret, self.torch.zeros_like(self._ret)),
+                 'final_length': self.torch.where(done_b, self._len, self.torch.zeros_like(self._len)),
+                 '_final': done_b.clone()}
+        self._ret.masked_fill_(done_b.unsqueeze(1), 0.0)
+        self._len.masked_fill_(done_b, 0)
         return obs, rew, term, trunc, infos
 
     def close(self):
