@@ -173,6 +173,7 @@ def main():
                     help='steps of the packed-obs + fused-projection measurement (default: --steps; 0 = off)')
     ap.add_argument('--cap', type=int, default=32, help='packed entries stored per agent row')
     ap.add_argument('--emb', type=int, default=96, help='fused projection width (obs_emb_size of RecurrentAC)')
+    ap.add_argument('--backend', default='nccl', help="torch.distributed backend for N > 1 ('nccl' = RCCL)")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-profile', action='store_true', help='no per-kernel HIP events in the timed region')
     args = ap.parse_args()
@@ -182,10 +183,15 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if os.environ.get('MFG_BENCH_SHARE_GPU') == '1':  # rehearsal of N ranks on fewer GPUs (not a bench number)
+        local = local % torch.cuda.device_count()
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(args.backend)
     from mfg_amd.spec import compile_spec
     from mfg_amd.engine import Engine, EV_MISC
     from mfg_amd.shard import env_range
