@@ -232,7 +232,7 @@ int mfg_decode_events(const uint8_t* ev_act, const uint8_t* ev_watch, const int3
 
 /* ---- observation output modes (the obs_dtype argument of mfg_reset / mfg_step) ---- */
 enum { MFG_OBS_F32 = 0, MFG_OBS_F64 = 1, MFG_OBS_PACKED = 2 };
-#define MFG_MAX_EMB 256
+#define MFG_MAX_EMB 128
 
 /* Packed observations + fused policy-input projection. With obs_dtype MFG_OBS_PACKED the
  * `obs` argument is a HOST pointer to this descriptor; its device buffers are the k = 0 rows and the engine
@@ -245,7 +245,7 @@ enum { MFG_OBS_F32 = 0, MFG_OBS_F64 = 1, MFG_OBS_PACKED = 2 };
  *   emb[a][j]      bias[j] + sum over ALL nonzero entries of val * wt[idx][j] (f32 fma in entry order): the
  *                  reference RecurrentAC.obs_proj (networks.py:19,52) evaluated without materialising the
  *                  dense row. wt = obs_proj.weight transposed, [lmax*h*w][emb_dim] row-major.
- * Any of idx/val (both or neither), count and emb may be NULL; emb needs wt and 0 < emb_dim <= MFG_MAX_EMB.
+ * Any of idx/val (both or neither), count and emb may be NULL; emb needs wt and 0 < emb_dim <= MFG_MAX_EMB (128).
  * lmax*h*w must be < 65536 (u16 idx). */
 typedef struct mfg_packed_obs {
   int32_t cap;        /* entries stored per agent row */

@@ -128,7 +128,7 @@ class MfgEvents(C.Structure):
 
 # observation output modes (include/mfg.h MFG_OBS_*) and the packed-obs descriptor
 OBS_F32, OBS_F64, OBS_PACKED = range(3)
-MAX_EMB = 256
+MAX_EMB = 128
 
 
 class MfgPackedObs(C.Structure):
