@@ -355,7 +355,11 @@ def main():
                              "valu_per_cu_cycle": round(c['SQ_INSTS_VALU'] / cu_cycles, 3),
                              "salu_per_cu_cycle": round(c['SQ_INSTS_SALU'] / cu_cycles, 3),
                              "lds_per_cu_cycle": round(c['SQ_INSTS_LDS'] / cu_cycles, 3),
-                             "wait_any_frac": c.get('wait_any_frac')}
+                             "wait_any_frac": c.get('wait_any_frac'),
+                             "lds_array_busy": round(c['SQ_LDS_IDX_ACTIVE'] / cu_cycles, 3)
+                             if c.get('SQ_LDS_IDX_ACTIVE') is not None else None,
+                             "lds_bank_conflict_share": round(c['SQ_LDS_BANK_CONFLICT'] / c['SQ_LDS_IDX_ACTIVE'], 3)
+                             if c.get('SQ_LDS_IDX_ACTIVE') else None}
         step_bytes = core_bytes(spec) + obs_bytes  # C3: 415 + 10,976 = ALGO_BYTES_PER_ENV_STEP
         pipe_bytes = step_bytes * B * k_call
         if dom:

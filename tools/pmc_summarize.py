@@ -30,12 +30,13 @@ def main():
     out = Path(sys.argv[4]) if len(sys.argv) > 4 else ROOT / 'profiles' / f'pmc_{tag}.json'
     base = ROOT / 'gpurun_out'
     sq, fe, wr = load(base / f'pmc_{tag}_sq'), load(base / f'pmc_{tag}_fetch'), load(base / f'pmc_{tag}_write')
+    lds = load(base / f'pmc_{tag}_lds') if (base / f'pmc_{tag}_lds').exists() else {}
     kernels, hbm = {}, {}
     for k in sorted(set(sq) | set(fe) | set(wr)):
         if not k.startswith('k_'):
             continue
         d = {}
-        for src in (sq, fe, wr):
+        for src in (sq, fe, wr, lds):
             for c, vals in src.get(k, {}).items():
                 d[c] = sum(vals) / len(vals)
         if 'FETCH_SIZE' in d and 'WRITE_SIZE' in d:
