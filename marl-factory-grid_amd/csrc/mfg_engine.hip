@@ -405,7 +405,6 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
   // (idx <= 560) the raw words of the next chunk are loaded one chunk ahead, so whether this chunk's
   // words are already in yw follows from idx alone (a twisted state had idx >= 624 > 560).
   uint32_t yw = idx <= 560 ? mt[idx + lane] : 0u;
-  int sh = 0, lowb = 0x7FFFFFFF;  // width region of icur: k = 32 - sh = bitlen(icur + 1), ranks (lowb, icur]
   while (icur >= lo) {
     if (idx > 560) {
       if (idx >= 624) {
@@ -429,12 +428,8 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
     // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
     // start the next chunk). So every chunk takes the same branch-free path, power-of-two crossings
     // and the i < 64 tail included.
-    // the width region is recomputed only when the previous chunk ended it (icur reached its low bound)
-    if (icur <= lowb) {
-      sh = __clz(icur + 1);
-      lowb = max(lo, (int)(0x80000000u >> sh) - 1);
-    }
-    const int span = icur - lowb;  // highest rank at width k
+    const int sh = __clz(icur + 1);
+    const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
     uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
@@ -467,8 +462,7 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
     // icur - j_s (rejected lanes sharing that rank carry no swap and may take the value harmlessly).
     // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
     // and pointer jumping resolves the chains.
-    // inext < j < i, i.e. j - inext - 1 < i - inext - 1 = nacc - A - 1 as unsigned (accepted lanes: A < nacc)
-    u64 cm = ballot((uint32_t)(j - inext - 1) < (uint32_t)(nacc - A - 1)) & m;
+    u64 cm = ballot(j > inext) & ballot(j < i) & m;
     if (cm) {
       if (popc(cm) <= RP_SERIAL_FWD) {
         do {
