@@ -101,6 +101,11 @@ struct MfgDevSpec {
   const int8_t* ray_pts;     // [nrays][maxpts][2] (dx, dy), padded
   const uint8_t* ray_len;    // [nrays]
   const uint32_t* ray_diag;  // [nrays] bit p: point p is a diagonal step from point p-1 (ray_caster.py:89-96)
+  // [nf][nrays][3] per ray origin (floor index) and ray: the light-blocking bits of its points that depend
+  // only on the static level (bit p: a wall at point p; a diagonal cut between two walls at step p), and
+  // the points whose blocking depends on a door (recomputed from the cell map at render time). Null:
+  // every point is tested at render time.
+  const uint32_t* ray_static;
   int32_t n_wd_pairs;        // static identifier collisions Wall[k]/Door[k] that one ray fan can reach
   const int32_t* wd_pairs;   // [n_wd_pairs][3]: k, wall cell, door cell
   uint64_t pcg_init_hi, pcg_init_lo, pcg_inc_hi, pcg_inc_lo;  // default_rng(env_seed) state after seeding

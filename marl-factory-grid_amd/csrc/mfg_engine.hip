@@ -2252,6 +2252,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     const int ax = rl(agx, a), ay = rl(agy, a);
     const int ox = rl(orgx, a), oy = rl(orgy, a);
     const int wx0 = full ? 0 : ax - S->r, wy0 = full ? 0 : ay - S->r;
+    const int ofl = S->ray_static ? uni((int)S->cell_f[ox * W + oy]) : -1;  // origin floor index (static table)
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
@@ -2275,13 +2276,34 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // mask keeps the corner test only on diagonal steps: cut when both orthogonal neighbours block
       // light (ray_caster.py:89-96)
       uint32_t blkm = 0, cutm = 0;
+      if (ofl >= 0) {
+        // the wall part from the per-origin table; only points next to doors are tested here (the door's
+        // present/closed state lives in the cell map)
+        const bool has = ray_id < S->nrays;
+        const uint32_t* rs = S->ray_static + ((size_t)ofl * S->nrays + (has ? ray_id : 0)) * 3;
+        blkm = has ? rs[0] : 0u;
+        cutm = has ? rs[1] : 0u;
+        uint32_t dyn = has ? rs[2] : 0u;
+        while (dyn) {
+          const int p = __ffs((int)dyn) - 1;
+          dyn &= dyn - 1;
+          const int8_t* pt = S->ray_pts + ((size_t)ray_id * S->maxpts + p) * 2;
+          const int x = ox + pt[0], y = oy + pt[1];
+          blkm |= light_block_bf<MM>(e, x, y) ? (1u << p) : 0u;
+          if (p > 0 && ((ray.diag >> p) & 1u)) {
+            const bool c = light_block_bf<MM>(e, x, oy + pt[-1]) & light_block_bf<MM>(e, ox + pt[-2], y);
+            cutm |= c ? (1u << p) : 0u;
+          }
+        }
+      } else {
 #pragma unroll
-      for (int p = 0; p < MAXPTS; p++) {
-        const int x = ox + ray.dx(p), y = oy + ray.dy(p);
-        blkm |= light_block_bf<MM>(e, x, y) ? (1u << p) : 0u;
-        if (p > 0) {
-          const bool c = light_block_bf<MM>(e, x, oy + ray.dy(p - 1)) & light_block_bf<MM>(e, ox + ray.dx(p - 1), y);
-          cutm |= c ? (1u << p) : 0u;
+        for (int p = 0; p < MAXPTS; p++) {
+          const int x = ox + ray.dx(p), y = oy + ray.dy(p);
+          blkm |= light_block_bf<MM>(e, x, y) ? (1u << p) : 0u;
+          if (p > 0) {
+            const bool c = light_block_bf<MM>(e, x, oy + ray.dy(p - 1)) & light_block_bf<MM>(e, ox + ray.dx(p - 1), y);
+            cutm |= c ? (1u << p) : 0u;
+          }
         }
       }
       cutm &= ray.diag;
@@ -3323,6 +3345,33 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   rc |= upload(e, rp.data(), rp.size(), &h.ray_pts);
   rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
   rc |= upload(e, rdiag.data(), rdiag.size(), &h.ray_diag);
+  {  // static light-blocking table per (origin floor cell, ray): walls only; door-dependent points flagged
+    const size_t n = (size_t)s->n_floor * h.nrays * 3;
+    h.ray_static = nullptr;
+    if (n * 4 <= ((size_t)256 << 20) && !getenv("MFG_NO_RAY_STATIC")) {
+      std::vector<uint32_t> rs(n, 0u);
+      auto wall = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && s->level[x * s->W + y] == 1; };
+      auto door = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && door_of[x * s->W + y] != 0xFF; };
+      for (int f = 0; f < s->n_floor; f++) {
+        const int ox = s->floor_cells[f] / s->W, oy = s->floor_cells[f] % s->W;
+        for (int r = 0; r < h.nrays; r++) {
+          uint32_t* o = &rs[((size_t)f * h.nrays + r) * 3];
+          for (int p = 0; p < rlen[r]; p++) {
+            const int x = ox + rp[((size_t)r * h.maxpts + p) * 2], y = oy + rp[((size_t)r * h.maxpts + p) * 2 + 1];
+            if (wall(x, y)) o[0] |= 1u << p;
+            else if (door(x, y)) o[2] |= 1u << p;
+            if (p > 0 && ((rdiag[r] >> p) & 1)) {
+              const int px = ox + rp[((size_t)r * h.maxpts + p - 1) * 2], py = oy + rp[((size_t)r * h.maxpts + p - 1) * 2 + 1];
+              const bool w1 = wall(x, py), w2 = wall(px, y), d1 = door(x, py), d2 = door(px, y);
+              if (w1 && w2) o[1] |= 1u << p;
+              else if ((w1 || d1) && (w2 || d2)) o[2] |= 1u << p;
+            }
+          }
+        }
+      }
+      rc |= upload(e, rs.data(), rs.size(), &h.ray_static);
+    }
+  }
   rc |= upload(e, base_map.data(), base_map.size(), &h.base_map);
   rc |= upload(e, base_map8.data(), base_map8.size(), &h.base_map8);
   rc |= upload(e, cell_f.data(), cell_f.size(), &h.cell_f);
