@@ -2330,6 +2330,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     sup.wx0 = wx0; sup.wy0 = wy0; sup.oh = oh; sup.ow = ow; sup.W = W;
     sup.wsup = wsup;
     sup.dsup = dsup;
+#ifdef MFG_ABLATE_OB_NOPAIRTEST
+    if (0)
+#endif
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
       // the first pass's pair cells stay in registers across agents (the usual single pass)
