@@ -141,4 +141,7 @@ struct MfgDevSpec {
   uint32_t comb_unit_tags[MFG_MAX_AGENTS];
   uint64_t comb_agents[MFG_MAX_AGENTS];
   const MfgLayerRec* lrec;   // [A][lmax] layer records
+  // rules that act in each step phase, in rule order (spawn rules and the like act only at reset)
+  int32_t n_ph[3];                       // tick_step, tick_post_step, on_check_done
+  uint8_t ph_rule[3][MFG_MAX_RULES];
 };

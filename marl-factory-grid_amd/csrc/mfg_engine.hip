@@ -2551,13 +2551,12 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
     do_action(e, o, a, slot);
     if (e.lane == a) o.my_slot = slot;
   }
-  const int nr = S->s.n_rules;
   if (!o.crashed)
-    for (int r = 0; r < nr && !o.crashed; r++) rule_tick_step<RNG, MAINT>(e, o, r, scratch);
+    for (int q = 0; q < S->n_ph[0] && !o.crashed; q++) rule_tick_step<RNG, MAINT>(e, o, S->ph_rule[0][q], scratch);
   if (!o.crashed)
-    for (int r = 0; r < nr && !o.crashed; r++) rule_post_step(e, o, r);
+    for (int q = 0; q < S->n_ph[1] && !o.crashed; q++) rule_post_step(e, o, S->ph_rule[1][q]);
   if (!o.crashed)
-    for (int r = 0; r < nr; r++) rule_check_done(e, o, r);
+    for (int q = 0; q < S->n_ph[2]; q++) rule_check_done(e, o, S->ph_rule[2][q]);
   // the step's membership-only shuffles stay as debt: paid by k_replay after the launch, or inline by
   // the next order-dependent consumer (spawn / reset)
   if (o.crashed || e.H(H_OVERFLOW)) {  // H_CRASHED keeps the reason (MFG_CRASH_*, include/mfg.h)
@@ -3244,6 +3243,20 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   for (int j = 0; j < s->n_dest_entries; j++) dest_list = std::max(dest_list, s->dest_entry_q[j] ? 2 * s->n_floor : 64);
   h.scratch_bytes = align_up(std::max({2048, 12 * (dirt_q + 2) + 16, 2 * (h.path_cap + 2), 128 + dest_list + 64}), 16);
   make_layout(s, &h.L, imax, pmax, dropmax, destmax, mmax, kmax, h.mstate_ints, h.path_cap, moving, h.dirt_cap);
+  // per-phase rule lists (rule_tick_step / rule_post_step / rule_check_done act only for these ops)
+  for (int r = 0; r < s->n_rules; r++) {
+    const int op = s->rules[r].op;
+    const bool tick = op == MFG_RULE_DOOR_AUTOCLOSE || op == MFG_RULE_RESPAWN_ITEMS || op == MFG_RULE_BATTERY_DECHARGE ||
+                      op == MFG_RULE_DONE_BATTERY || op == MFG_RULE_RESPAWN_DIRT || op == MFG_RULE_MOVE_MAINTAINERS ||
+                      op == MFG_RULE_DEST_REACH || op == MFG_RULE_DONE_DEST;
+    const bool post = op == MFG_RULE_RESPAWN_ITEMS || op == MFG_RULE_WATCH_COLLISIONS || op == MFG_RULE_BATTERY_DECHARGE ||
+                      op == MFG_RULE_DONE_BATTERY;
+    const bool done = op == MFG_RULE_DONE_MAXSTEPS || op == MFG_RULE_WATCH_COLLISIONS || op == MFG_RULE_DONE_BATTERY ||
+                      op == MFG_RULE_DONE_MAINT_COLLISION || op == MFG_RULE_DONE_DIRT || op == MFG_RULE_DONE_DEST;
+    if (tick) h.ph_rule[0][h.n_ph[0]++] = (uint8_t)r;
+    if (post) h.ph_rule[1][h.n_ph[1]++] = (uint8_t)r;
+    if (done) h.ph_rule[2][h.n_ph[2]++] = (uint8_t)r;
+  }
   h.step_rng = 0;
   for (int r = 0; r < s->n_rules; r++)  // dirt spawns and maintainer retargets consume the floor order mid-step
     if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT || s->rules[r].op == MFG_RULE_MOVE_MAINTAINERS) h.step_rng = 1;
