@@ -775,6 +775,43 @@ __device__ int colliders_lanes(const Env& e, int cell) {
   return ok ? n : 0;
 }
 
+// Per door (lane = door, returned for lanes < nd): the number of entities in the global pos_dict at its cell
+// (all = global_count) or of its colliders (coll = colliders_at), by one lane-parallel LDS histogram per
+// entity table instead of a uniform loop over every table per door. cnt: >= 64 ints of LDS scratch.
+__device__ int door_cell_counts(const Env& e, int* cnt, bool coll) {
+  SpecP S = e.S;
+  const int lane = e.lane, nd = S->nd, HW = S->HW;
+  if (lane < nd) {
+    const int w = e.door()[lane];
+    cnt[lane] = coll ? ((w & DW_PRESENT) && !(w & DW_OPEN) ? 1 : 0) : ((w & DW_PRESENT) ? 1 : 0);
+  }
+  wave_sync();
+  auto add = [&](int cell) {  // cell < 0 or off-grid: nothing
+    const int d = ((unsigned)cell < (unsigned)HW) ? S->door_of[cell] : 0xFF;
+    if (d != 0xFF) atomicAdd(&cnt[d], 1);
+  };
+  if (lane < S->A) add(e.agpos()[lane]);
+  auto grp = [&](const int* tbl, int n) {
+    for (int i = lane; i < n; i += MFG_WAVE) {
+      const int w = tbl[i];
+      if (w & EW_PRESENT) add(EW_POS(w));
+    }
+  };
+  if (!coll) {
+    grp(e.items(), e.H(H_N_ITEMS));
+    grp(e.pods(), e.H(H_N_PODS));
+    grp(e.drops(), e.H(H_N_DROPS));
+    grp(e.dests(), e.H(H_N_DESTS));
+    grp(e.dirtpos(), e.H(H_N_DIRT));
+    if (S->mmax) grp(e.machines(), e.H(H_N_MACHINES));
+  }
+  if (S->kmax) grp(e.maints(), e.H(H_N_MAINTS));
+  wave_sync();
+  const int n = lane < nd ? cnt[lane] : 0;
+  wave_sync();
+  return n;
+}
+
 // ------------------------------------------------------------------------------------------------
 // spawn-position queries (global_entities.py:77-121)
 // ------------------------------------------------------------------------------------------------
@@ -1543,7 +1580,7 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
   if (op == MFG_RULE_DOOR_AUTOCLOSE) {  // doors/rules.py:20-28, doors/entitites.py:107-122
     if (S->nd > 0) {
       const int nd = S->nd;
-      const int cnt = global_count_lanes(e, e.lane < nd ? S->door_cells[e.lane < nd ? e.lane : 0] : -1);  // lane = door
+      const int cnt = door_cell_counts(e, e.scratch, false);  // lane = door: len(pos_dict[door])
       wave_sync();
       if (e.lane < nd) {
         int w = e.door()[e.lane];
@@ -1676,9 +1713,15 @@ __device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
     // candidate cells first, lane-parallel (lane = door, then lane = agent); the ordered passes below
     // visit only cells with >= 2 colliders (usually none)
     const int nd = S->nd;
-    const u64 dcand = ballot(e.lane < nd && colliders_lanes(e, e.lane < nd ? S->door_cells[e.lane < nd ? e.lane : 0] : -1) >= 2);
+    const int dcnt = nd ? door_cell_counts(e, e.scratch, true) : 0;  // whole wave: every lane adds its entities
+    const u64 dcand = ballot(e.lane < nd && dcnt >= 2);
     const int myp = e.lane < A ? e.agpos()[e.lane] : -1;
-    const u64 acand = ballot(e.lane < A && door_idx(e, myp < 0 ? 0 : myp) < 0 && colliders_lanes(e, myp) >= 2);
+    // agents on non-door cells: the other agents on the same cell (readlane loop) + maintainers there
+    int na = 0;
+    for (int b = 0; b < A; b++) na += (rl(myp, b) == myp) ? 1 : 0;
+    const int nkm = S->kmax ? e.H(H_N_MAINTS) : 0;
+    for (int k = 0; k < nkm; k++) { const int w = e.maints()[k]; na += (EW_POS(w) == myp && (w & EW_PRESENT)) ? 1 : 0; }
+    const u64 acand = ballot(e.lane < A && door_idx(e, myp < 0 ? 0 : myp) < 0 && na >= 2);
     for (u64 dm = dcand; dm; dm &= dm - 1) {
       const int d = ffs64(dm);
       const int cell = S->door_cells[d];
@@ -2703,7 +2746,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
   if (full) {
     env_full(S, slice, e, env);
   } else {
-    e.S = S; e.lds = slice; e.scratch = nullptr; e.stab = nullptr; e.cmap = nullptr;
+    e.S = S; e.lds = slice; e.scratch = (int*)(slice + ((S->L.o_mt + 15) & ~15)); e.stab = nullptr; e.cmap = nullptr;
     e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
   }
   uint8_t* rec = state + (size_t)env * S->L.size;
@@ -3281,7 +3324,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     h.max_pairs = std::max(16, 2 * tot_cap + 3 * tot_cap);
   }
   h.pair_pool = nullptr;
-  h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16);
+  h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16) + 4 * MFG_WAVE;  // + per-door count scratch
   h.fv_words = align_up((2 * h.fr + 1) * (2 * h.fr + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
