@@ -128,6 +128,7 @@ struct MfgDevSpec {
   int32_t max_pairs;         // capacity of the obs identifier-collision pair list (bounded by group sizes)
   int32_t pairs_lds;         // pairs held in the k_obs LDS slice; the rest go to pair_pool
   int32_t* pair_pool;        // [B][max_pairs - pairs_lds][3] HBM spill of the pair list, or null
+  int32_t* rd_list;          // [2][B + 2]: per step parity, [0] = count, [2..] = envs k_logic flagged done (auto-reset)
   const int16_t* cell_f;     // [HW] floor index of a cell, -1 for walls
   const uint8_t* node_ok;    // [nf] floor cell has a floor 8-neighbour (a node of points_to_graph)
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)

@@ -2734,7 +2734,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
                                                         const int32_t* actions, unsigned philox_seed,
                                                         unsigned env_base, long long step, double* reward,
                                                         uint8_t* done, uint8_t* ev_act, uint8_t* ev_watch,
-                                                        int32_t* ev_misc, int auto_reset) {
+                                                        int32_t* ev_misc, int auto_reset, int rd_slot) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = threadIdx.x >> 6;  // (a uniform wid here measured slower: 0.319 vs 0.298 ms at C3)
@@ -2777,7 +2777,14 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
   StepOut o;
   env_step<FULL, MAINT>(e, my_act, o, e.scratch);
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
-  if (o.done && auto_reset) e.setH(H_DONE, 1);
+  if (o.done && auto_reset) {
+    e.setH(H_DONE, 1);
+    // append to this step's done list (k_resetdone walks it instead of one wave per env)
+    int32_t* lst = S->rd_list + (size_t)rd_slot * (size_t)(B + 2);
+    if (e.lane == 0) lst[2 + atomicAdd(&lst[0], 1)] = (int32_t)env;
+  }
+  // the next step's list is empty: its last reader (the previous step's k_resetdone) has finished
+  if (blockIdx.x == 0 && threadIdx.x == 0) S->rd_list[(size_t)(rd_slot ^ 1) * (size_t)(B + 2)] = 0;
   wave_sync();
   if (one_pass) {
     if (e.lane < (bytes >> 4)) {
@@ -2789,23 +2796,32 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, ui
   }
 }
 
-// Auto-reset of the envs k_logic flagged (H_DONE): pays the shuffle debt, then Factory.reset().
-__global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B) {
+// Auto-reset of the envs k_logic flagged (H_DONE) in this step's done list: pays the shuffle debt, then
+// Factory.reset(). A fixed grid of waves strides over the list (count <= B, every wave exits), so a step
+// with few episode ends costs a few waves instead of one wave per env.
+__global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B,
+                                                            int rd_slot) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = uni(threadIdx.x >> 6);  // wave-uniform: slice and record addresses become scalar
-  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
-  if (env >= B) return;
-  uint8_t* rec = state + (size_t)env * S->L.size;
-  if (uni(((const int*)(rec + S->L.o_hdr))[H_DONE]) == 0) return;
-  Env e;
-  env_full(S, smem + (size_t)wid * S->lds_full, e, env);
-  rec_copy(e.lds, rec, S->L.size, e.lane);
-  wave_sync();
-  env_reset(e, e.scratch);
-  e.setH(H_DONE, 0);
-  wave_sync();
-  rec_copy(rec, e.lds, S->L.size, e.lane);
+  const int32_t* lst = S->rd_list + (size_t)rd_slot * (size_t)(B + 2);
+  const long long n = min((long long)uni(lst[0]), B);
+  const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+  for (long long q = (long long)blockIdx.x * (blockDim.x >> 6) + wid; q < n; q += nw) {
+    const long long env = uni(lst[2 + q]);
+    if (env < 0 || env >= B) continue;
+    uint8_t* rec = state + (size_t)env * S->L.size;
+    if (uni(((const int*)(rec + S->L.o_hdr))[H_DONE]) == 0) continue;
+    Env e;
+    env_full(S, smem + (size_t)wid * S->lds_full, e, env);
+    rec_copy(e.lds, rec, S->L.size, e.lane);
+    wave_sync();
+    env_reset(e, e.scratch);
+    e.setH(H_DONE, 0);
+    wave_sync();
+    rec_copy(rec, e.lds, S->L.size, e.lane);
+    wave_sync();
+  }
 }
 
 // Observation render of every env into obs[env] (read-only on the state). MM: the spec has machines or
@@ -2897,6 +2913,8 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
 // ================================================================================================
 // host side: C-ABI (include/mfg.h)
 // ================================================================================================
+static int wpb_for(size_t lds);  // waves per workgroup for a per-wave LDS slice (launch shape, below)
+
 struct mfg_engine {
   int device = 0;
   long long B = 0;
@@ -2908,6 +2926,10 @@ struct mfg_engine {
   // per-kernel timing (mfg_profile)
   bool prof = false;
   std::vector<hipEvent_t> ev_free;
+  int rd_slot = 0;
+  int rd_blocks = 1;  // k_resetdone workgroups (occupancy x CUs)  // done list k_logic appends to (alternates per step)
+  hipStream_t ov_stream = nullptr;  // MFG_ABLATE_OVERLAP measurement only (timing of a replay overlapped with the next call)
+  hipEvent_t ov_ev = nullptr;
   struct Mark { int k; hipEvent_t a, b; };
   std::vector<Mark> marks;
   std::string err;  // mfg_last_error(e)
@@ -3476,6 +3498,16 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     e->d_bufs.push_back(pool);
     h.pair_pool = (int*)pool;
   }
+  {  // auto-reset done lists, both empty
+    void* lst = nullptr;
+    const size_t bytes = (size_t)2 * 4 * ((size_t)n_envs + 2);
+    if (hipMalloc(&lst, bytes) != hipSuccess || hipMemset(lst, 0, bytes) != hipSuccess) {
+      if (lst) (void)hipFree(lst);
+      delete e; return fail("done list allocation failed");
+    }
+    e->d_bufs.push_back(lst);
+    h.rd_list = (int32_t*)lst;
+  }
   if (h.bfs_bytes && !h.bfs_off) {  // BFS scratch in HBM, one slice per env
     void* pool = nullptr;
     if (hipMalloc(&pool, (size_t)h.bfs_bytes * (size_t)n_envs) != hipSuccess) {
@@ -3484,11 +3516,20 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     e->d_bufs.push_back(pool);
     h.bfs_pool = (uint8_t*)pool;
   }
-  if ((h.bfs_pool || h.pair_pool) &&
-      hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
+  if (hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
     delete e; return fail("spec upload failed");
   }
   e->maxpts = h.maxpts;
+  {  // k_resetdone's grid: the waves resident at once (one round; each strides over the done list)
+    const int wpb = wpb_for(h.lds_full);
+    int per_cu = 0, n_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resetdone, wpb * 64, (size_t)h.lds_full * wpb) !=
+            hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+      delete e; return fail("occupancy query failed");
+    }
+    e->rd_blocks = std::max(1, per_cu) * std::max(1, n_cu);
+  }
   *out = e;
   return 0;
 }
@@ -3675,33 +3716,37 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset);
+                       auto_reset, e->rd_slot);
     } else if (e->h.step_rng) {
     hipLaunchKernelGGL((k_logic<true, false>), GEOM(e->h.lds_logic), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset);
+                       auto_reset, e->rd_slot);
     } else {
     hipLaunchKernelGGL((k_logic<false, false>), GEOM(e->h.lds_logic), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset);
+                       auto_reset, e->rd_slot);
     }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(std::string("k_logic launch: ") + hipGetErrorString(err));
     PROF_END(e, st, MFG_K_LOGIC);
     }
+    const int rd_cur = e->rd_slot;
+    e->rd_slot ^= 1;  // the next k_logic appends to the other list (and empties this one after k_resetdone)
     // measurement switch: pay the debt every step (before the resets) instead of once per call
     static const int replay_each = [] { const char* v = getenv("MFG_REPLAY_EACH_STEP"); return v ? atoi(v) : 0; }();
     if (replay_each && k + 1 < K && replay_impl(e, stream)) return -1;
     if (auto_reset) {
       PROF_BEGIN(e, st);
-      hipLaunchKernelGGL(k_resetdone, GEOM(e->h.lds_full), st,
-                         e->d_spec, e->d_state, (long long)e->B);
+      const int wpb = wpb_for(e->h.lds_full);
+      const long long nwg = std::min<long long>(env_grid(e, wpb), e->rd_blocks);
+      hipLaunchKernelGGL(k_resetdone, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, st,
+                         e->d_spec, e->d_state, (long long)e->B, rd_cur);
       hipError_t err = hipGetLastError();
       if (err != hipSuccess) return fail(std::string("k_resetdone launch: ") + hipGetErrorString(err));
       PROF_END(e, st, MFG_K_RESETDONE);
@@ -3711,6 +3756,19 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     if (obs && obs_dtype != MFG_OBS_PACKED && launch_obs(e, (uint8_t*)obs + (size_t)k * obs_row, obs_dtype, st))
       return -1;
 #endif
+  }
+  // measurement switch (results NOT exact: the replay races the next call's k_logic header write-back and
+  // k_resetdone; run with auto_reset = 0): the call's replay runs on a second stream, overlapped with the
+  // next call's kernels, to price a pipelined replay
+  static const int overlap = [] { const char* v = getenv("MFG_ABLATE_OVERLAP"); return v ? atoi(v) : 0; }();
+  if (overlap) {
+    if (!e->ov_stream) {
+      HIPCHK(hipStreamCreateWithFlags(&e->ov_stream, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&e->ov_ev, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(e->ov_ev, st));
+    HIPCHK(hipStreamWaitEvent(e->ov_stream, e->ov_ev, 0));
+    return replay_impl(e, e->ov_stream);
   }
   return replay_impl(e, stream);
 }
