@@ -142,7 +142,8 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
 }
 // In-place twist in its three dependency phases (i<227: old inputs; 227<=i<454: mt[i-227] new;
 // 454<=i<623: mt[i-227] new). Each phase issues all its LDS reads before any of its writes, so one
-// wave pays three LDS round trips per 624 draws.
+// wave pays three LDS round trips per 624 draws. (Taking mt[i+1] from the neighbour lane by DPP wave_shl
+// instead of a third LDS read was bit-exact and measured no faster: k_replay 11.05-11.12 vs 10.97-11.03 ms.)
 __device__ void mt_twist(const Env& e) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
@@ -3568,14 +3569,21 @@ static int wpb_for(size_t lds) { return (int)std::max<size_t>(1, std::min<size_t
 static unsigned env_grid(const mfg_engine* e, int wpb) { return (unsigned)((e->B + wpb - 1) / wpb); }
 // launch geometry of a kernel with `lds` bytes of dynamic LDS per wave
 #define GEOM(lds) dim3(env_grid(e, wpb_for(lds))), dim3(wpb_for(lds) * 64), (size_t)(lds) * wpb_for(lds)
+// waves per workgroup of k_logic / k_obs (overrides for measurements: MFG_LOGIC_WPB, MFG_OBS_WPB). k_logic runs
+// one wave per workgroup (C3: 0.1544 -> 0.1507 ms; its slot frees as soon as its env is done); k_obs keeps 4
+// (1 and 2 measured within noise, tools/wpb_sweep.sh)
+static int wpb_env(const char* name, int dflt) { const char* v = getenv(name); return v ? std::max(1, atoi(v)) : dflt; }
+static const int obs_wpb = wpb_env("MFG_OBS_WPB", MFG_WPB), logic_wpb = wpb_env("MFG_LOGIC_WPB", 1);
+#define GEOMW(lds, W) dim3(env_grid(e, std::min(W, wpb_for(lds)))), dim3(std::min(W, wpb_for(lds)) * 64), \
+    (size_t)(lds) * std::min(W, wpb_for(lds))
 
 template <int MP, typename OT, bool PK>
 static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipStream_t st) {
   if (e->h.mmax || e->h.kmax)
-    hipLaunchKernelGGL((k_obs<MP, OT, true, PK>), GEOM(e->h.lds_obs),
+    hipLaunchKernelGGL((k_obs<MP, OT, true, PK>), GEOMW(e->h.lds_obs, obs_wpb),
                        st, e->d_spec, e->d_state, (long long)e->B, obs, pk);
   else
-    hipLaunchKernelGGL((k_obs<MP, OT, false, PK>), GEOM(e->h.lds_obs),
+    hipLaunchKernelGGL((k_obs<MP, OT, false, PK>), GEOMW(e->h.lds_obs, obs_wpb),
                        st, e->d_spec, e->d_state, (long long)e->B, obs, pk);
   return hipGetLastError();
 }
@@ -3711,21 +3719,21 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     {
     PROF_BEGIN(e, st);
     if (e->h.bfs_bytes) {
-    hipLaunchKernelGGL((k_logic<true, true>), GEOM(e->h.lds_logic), st,
+    hipLaunchKernelGGL((k_logic<true, true>), GEOMW(e->h.lds_logic, logic_wpb), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
                        auto_reset, e->rd_slot);
     } else if (e->h.step_rng) {
-    hipLaunchKernelGGL((k_logic<true, false>), GEOM(e->h.lds_logic), st,
+    hipLaunchKernelGGL((k_logic<true, false>), GEOMW(e->h.lds_logic, logic_wpb), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
                        auto_reset, e->rd_slot);
     } else {
-    hipLaunchKernelGGL((k_logic<false, false>), GEOM(e->h.lds_logic), st,
+    hipLaunchKernelGGL((k_logic<false, false>), GEOMW(e->h.lds_logic, logic_wpb), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,

@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B timing of exact engine variants: tools/ab_run.sh VARIANT... (build/ablate/libmfg_hip_VARIANT.so, built by
+# tools/build_ablation.sh with -DMFG_<VARIANT>) against the in-tree library, alternating, 2 rounds each.
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+for r in 1 2; do
+  for v in base "$@"; do
+    lib=""; [ "$v" != base ] && lib="build/ablate/libmfg_hip_$v.so"
+    MFG_HIP_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --alt-steps 0 --packed-steps 0 --steps 800 \
+      --warmup 200 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
+    python -c "
+import json; d=json.load(open('gpurun_out/ab_$v.json'))
+print('$v', round(d['value']/1e6,2), {k: v['mean_launch_ms'] for k, v in d['roofline']['kernels'].items()})"
+  done
+done
