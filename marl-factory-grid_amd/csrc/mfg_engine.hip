@@ -464,12 +464,22 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
     // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
     // and pointer jumping resolves the chains.
     u64 cm = ballot(j > inext) & ballot(j < i) & m;
+#ifdef MFG_ABLATE_NOFWD
+    cm = 0;
+#endif
+#ifdef MFG_ABLATE_NOFWD_SERIAL
+    if (popc(cm) <= RP_SERIAL_FWD) cm = 0;
+#endif
+#ifdef MFG_ABLATE_NOFWD_TABLE
+    if (popc(cm) > RP_SERIAL_FWD) cm = 0;
+#endif
     if (cm) {
       if (popc(cm) <= RP_SERIAL_FWD) {
+        const int keyv = icur - j;  // the rank whose i equals this lane's j
         do {
           const int s = ffs64(cm);
-          cm &= ~(1ull << s);
-          const int key = icur - rl(j, s);
+          asm volatile("s_bitset0_b64 %0, %1" : "+s"(cm) : "s"(s));
+          const int key = rl(keyv, s);
           const int vs = rl(v, s);
           v = A == key ? vs : v;
         } while (cm);
