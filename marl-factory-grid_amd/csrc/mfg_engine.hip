@@ -2187,18 +2187,28 @@ __device__ int build_id_pairs(const Env& e, const PairList& pairs) {
       const bool has = me.id >= 0 && me.id < S->nd && (e.door()[me.id < S->nd && me.id >= 0 ? me.id : 0] & DW_PRESENT);
       emit(has, me.cell, has ? S->door_cells[me.id] : 0, code | (((K_DOOR << 12) | me.id) << 16));
     }
-    // dynamic-dynamic partners (different kinds, equal identifiers): entity b+lane pairs with every later one
-    for (int j = b + 1; j < tot; j++) {
-      IdEnt o;
-      if (j < b + MFG_WAVE) {
-        const int jl = j - b;
-        o.kind = rl(me.kind, jl); o.slot = rl(me.slot, jl); o.cell = rl(me.cell, jl); o.id = rl(me.id, jl);
-      } else {
-        o = id_entity<MM>(e, j, nI, nP, nR, nS, nT, nM, tot);
-      }
-      const bool has = b + lane < j && me.id >= 0 && o.id == me.id && o.kind != me.kind;
-      emit(has, me.cell, o.cell, code | (((o.kind << 12) | o.slot) << 16));
-    }
+    // dynamic-dynamic partners (different kinds, equal identifiers), oriented (earlier, later) in the
+    // enumeration order items, pods, drop-offs, destinations, dirt, machines, maintainers. Every kind but dirt
+    // numbers its identifiers base + slot, so the partner of kind k2 is slot id - base(k2): one lookup per
+    // kind instead of a loop over all later entities. Non-dirt pairs are emitted from their earlier member,
+    // dirt pairs from the dirt pile.
+    const int mord = me.id < 0 ? -1 : (me.kind == K_ITEM ? 0 : me.kind == K_POD ? 1 : me.kind == K_DROP ? 2 :
+                                       me.kind == K_DEST ? 3 : me.kind == K_DIRT ? 4 : me.kind == K_MACHINE ? 5 : 6);
+    auto partner = [&](int k2, int o2, const int* tbl, int n2, int base2) {
+      const int l2 = me.id - base2;
+      const bool inr = mord >= 0 && o2 != mord && (unsigned)l2 < (unsigned)n2;
+      const int w2 = tbl[inr ? l2 : 0];
+      const bool later = o2 > mord;
+      const bool has = inr && (w2 & EW_PRESENT) && (later || mord == 4);
+      const int c2 = EW_POS(w2), code2 = (k2 << 12) | (inr ? l2 : 0);
+      emit(has, later ? me.cell : c2, later ? c2 : me.cell, later ? (code | (code2 << 16)) : (code2 | (code << 16)));
+    };
+    if (nI) partner(K_ITEM, 0, e.items(), nI, e.H(H_ITEM_BASE));
+    if (nP) partner(K_POD, 1, e.pods(), nP, e.H(H_POD_BASE));
+    if (nR) partner(K_DROP, 2, e.drops(), nR, e.H(H_DROP_BASE));
+    if (nS) partner(K_DEST, 3, e.dests(), nS, e.H(H_DEST_BASE));
+    if (nM) partner(K_MACHINE, 5, e.machines(), nM, e.H(H_MACHINE_BASE));
+    if (nK) partner(K_MAINT, 6, e.maints(), nK, e.H(H_MAINT_BASE));
   }
   // static Wall[k] / Door[k] pairs (host-filtered to pairs one ray fan can reach)
   for (int q0 = 0; q0 < S->n_wd_pairs; q0 += MFG_WAVE) {
