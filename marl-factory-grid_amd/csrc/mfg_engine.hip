@@ -2562,7 +2562,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         // for these stores (1.00x with MFG_OBS_NT=0): the 49-lane layer rows are not 64-B aligned.
         // Packing rows into aligned 64-lane stores (ds_bpermute) cut that to 1.14x but cost 67 VGPRs
         // and k_obs 0.494 -> 0.543 ms, so it was dropped (k_obs).
-#if MFG_OBS_NT
+#if defined(MFG_ABLATE_OB_NOSTORE)  // timing only: the values are computed, (almost) never stored
+        if (inwin && out == (OT)-12345.0) out_a[(size_t)l * dd + wi] = out;
+#elif MFG_OBS_NT
         if (inwin) __builtin_nontemporal_store(out, &out_a[(size_t)l * dd + wi]);
 #else
         if (inwin) out_a[(size_t)l * dd + wi] = out;
