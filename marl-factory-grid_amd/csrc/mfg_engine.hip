@@ -2642,23 +2642,23 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
     if (ev_act) ev_act[row * A + e.lane] = (uint8_t)o.my_act_ev;
     if (ev_watch) ev_watch[row * A + e.lane] = (uint8_t)o.my_watch_ev;
   }
-  if (e.lane == 0) {
-    if (done) done[row] = (uint8_t)o.done;
-    if (ev_misc) {
-      int32_t* m = ev_misc + row * MFG_EV_MISC;
-      m[0] = (int32_t)(uint32_t)o.door_coll;
-      m[1] = (int32_t)(uint32_t)(o.door_coll >> 32);
-      m[2] = o.respawn_items_value;
-      m[3] = o.dirt_spawn_value;
-      m[4] = o.dirt_spawn_valid;
-      m[5] = o.dest_reached;
-      m[6] = (o.door_autoclose ? 1 : 0) | (o.crashed ? 2 : 0) | ((o.crashed & 0xFF) << 8);
-      m[7] = o.done_mask;
-      m[8] = e.hdr()[H_STEP];
-      m[9] = e.hdr()[H_EPISODE];
-      m[10] = (int32_t)o.maint_coll;
-      m[11] = e.S->kmax ? e.hdr()[H_MAINT_BASE] : 0;
-    }
+  if (e.lane == 0 && done) done[row] = (uint8_t)o.done;
+  if (ev_misc) {  // one 12-lane store (lane k writes slot k) instead of 12 single-lane stores
+    const int l = e.lane;
+    int v = (int)(uint32_t)o.door_coll;
+    v = l == 1 ? (int)(uint32_t)(o.door_coll >> 32) : v;
+    v = l == 2 ? o.respawn_items_value : v;
+    v = l == 3 ? o.dirt_spawn_value : v;
+    v = l == 4 ? o.dirt_spawn_valid : v;
+    v = l == 5 ? o.dest_reached : v;
+    v = l == 6 ? ((o.door_autoclose ? 1 : 0) | (o.crashed ? 2 : 0) | ((o.crashed & 0xFF) << 8)) : v;
+    v = l == 7 ? o.done_mask : v;
+    v = l == 8 ? e.hdr()[H_STEP] : v;
+    v = l == 9 ? e.hdr()[H_EPISODE] : v;
+    v = l == 10 ? (int32_t)o.maint_coll : v;
+    v = l == 11 ? (e.S->kmax ? e.hdr()[H_MAINT_BASE] : 0) : v;
+    static_assert(MFG_EV_MISC == 12, "ev_misc row width");
+    if (e.lane < MFG_EV_MISC) ev_misc[row * MFG_EV_MISC + e.lane] = v;
   }
 }
 
