@@ -2882,26 +2882,20 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, cons
   if (e.lane == 0 && e.hdrp[H_OVERFLOW]) ((int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_OVERFLOW] = 1;
 }
 
-// Pay every env's pending floor-shuffle debt. Touches only the header, MT state and floor permutation
-// of each record, so it runs at high occupancy.
-__global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, uint8_t* state, long long B) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  SpecP S = (SpecP)S_;
-  const int wid = uni(threadIdx.x >> 6);  // wave-uniform: the slice addresses become scalar
-  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
-  if (env >= B) return;
-  uint8_t* rec = state + (size_t)env * S->L.size;
+// Pay one env's pending floor-shuffle debt in a k_replay-sized LDS slice. Touches only the header, MT state
+// and floor permutation of the record, so it runs at high occupancy.
+__device__ __forceinline__ void replay_env(SpecP S, uint8_t* slice, uint8_t* rec) {
   const int debt = ((const int*)(rec + S->L.o_hdr))[H_DEBT];
   if (debt == 0) return;
   // LDS slice laid out like the record prefix so Env accessors work: [hdr .. o_mt .. o_perm end]
   Env e;
   e.S = S;
-  e.lds = smem + (size_t)wid * S->lds_replay_per_wave - S->L.o_mt + 4 * RP_HDR_N;
+  e.lds = slice - S->L.o_mt + 4 * RP_HDR_N;
   e.lane = lane_id();
-  e.scratch = (int*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_sink_off);
+  e.scratch = (int*)(slice + S->replay_sink_off);
   e.cmap = nullptr;
-  e.stab = (uint32_t*)(smem + (size_t)wid * S->lds_replay_per_wave + S->replay_stab_off);
-  e.hdrp = (int*)(smem + (size_t)wid * S->lds_replay_per_wave);
+  e.stab = (uint32_t*)(slice + S->replay_stab_off);
+  e.hdrp = (int*)slice;
   int* hdr = e.hdr();
   const int n16 = S->replay_mtperm >> 4;  // MT + u16 perm image of the record, 16 B units
   if (e.lane < RP_HDR_N) hdr[e.lane] = ((const int*)(rec + S->L.o_hdr))[e.lane];
@@ -2914,8 +2908,8 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   wave_sync();
   if (S->xchg_ordered) {
 #ifndef MFG_ABLATE_NODEBT
-    const int debt = e.H(H_DEBT);
-    for (int k = 0; k < debt; k++) replay_shuffle(e, e.perm());
+    const int d = e.H(H_DEBT);
+    for (int k = 0; k < d; k++) replay_shuffle(e, e.perm());
 #endif
     e.setH(H_DEBT, 0);
     wave_sync();
@@ -2930,6 +2924,35 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   if (e.lane == 0) {
     ((int*)(rec + S->L.o_hdr))[H_DEBT] = 0;
     ((int*)(rec + S->L.o_hdr))[H_MT_IDX] = hdr[H_MT_IDX];
+  }
+  wave_sync();
+}
+
+// Pay every env's pending floor-shuffle debt (once per mfg_step call).
+__global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, uint8_t* state, long long B) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const int wid = uni(threadIdx.x >> 6);  // wave-uniform: the slice addresses become scalar
+  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
+  if (env >= B) return;
+  replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
+}
+
+// The same for the envs on a step's done list, before k_resetdone resets them: their debt is paid at
+// k_replay's occupancy instead of inside the reset kernel's much larger slice. A grid of resident waves
+// strides over the list (every wave exits).
+__global__ void __launch_bounds__(MFG_WPB * 64) k_replay_done(const MfgDevSpec* S_, uint8_t* state, long long B,
+                                                              int rd_slot) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const int wid = uni(threadIdx.x >> 6);
+  const int32_t* lst = S->rd_list + (size_t)rd_slot * (size_t)(B + 2);
+  const long long n = min((long long)uni(lst[0]), B);
+  const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+  for (long long q = (long long)blockIdx.x * (blockDim.x >> 6) + wid; q < n; q += nw) {
+    const long long env = uni(lst[2 + q]);
+    if (env < 0 || env >= B) continue;
+    replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
   }
 }
 
@@ -2949,8 +2972,9 @@ struct mfg_engine {
   // per-kernel timing (mfg_profile)
   bool prof = false;
   std::vector<hipEvent_t> ev_free;
-  int rd_slot = 0;
-  int rd_blocks = 1;  // k_resetdone workgroups (occupancy x CUs)  // done list k_logic appends to (alternates per step)
+  int rd_slot = 0;     // done list k_logic appends to (alternates per step)
+  int rd_blocks = 1;   // k_resetdone workgroups (occupancy x CUs)
+  int rpd_blocks = 1;  // k_replay_done workgroups (one wave each)
   hipStream_t ov_stream = nullptr;  // MFG_ABLATE_OVERLAP measurement only (timing of a replay overlapped with the next call)
   hipEvent_t ov_ev = nullptr;
   struct Mark { int k; hipEvent_t a, b; };
@@ -3552,6 +3576,11 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
       delete e; return fail("occupancy query failed");
     }
     e->rd_blocks = std::max(1, per_cu) * std::max(1, n_cu);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_replay_done, 64, (size_t)h.lds_replay_per_wave) !=
+        hipSuccess) {
+      delete e; return fail("occupancy query failed");
+    }
+    e->rpd_blocks = std::max(1, per_cu) * std::max(1, n_cu);
   }
   *out = e;
   return 0;
@@ -3773,6 +3802,9 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     if (replay_each && k + 1 < K && replay_impl(e, stream)) return -1;
     if (auto_reset) {
       PROF_BEGIN(e, st);
+      // the done envs' debt first, at k_replay's occupancy; k_resetdone then finds none left to pay
+      hipLaunchKernelGGL(k_replay_done, dim3((unsigned)std::min<long long>(e->B, e->rpd_blocks)), dim3(64),
+                         (size_t)e->h.lds_replay_per_wave, st, e->d_spec, e->d_state, (long long)e->B, rd_cur);
       const int wpb = wpb_for(e->h.lds_full);
       const long long nwg = std::min<long long>(env_grid(e, wpb), e->rd_blocks);
       hipLaunchKernelGGL(k_resetdone, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, st,
