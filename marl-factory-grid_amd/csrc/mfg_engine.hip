@@ -389,16 +389,18 @@ static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice")
 #endif
 // TOP14: every width k = bitlen(i + 1) is <= 14 (nf < 16384), so r = y >> (32 - k) reads only bits
 // 18..31 of the tempered word, which the last tempering step (y ^= y >> 18) leaves unchanged.
-template <bool TOP14>
-__device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
+// SWAP = false: the draws of a shuffle of hi + 1 elements only (randbelow(i + 1) for i = hi .. 1, no
+// permutation), e.g. shuffle(empty_positions) in the reset, on the same chunked path.
+template <bool TOP14, bool SWAP = true>
+__device__ void replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
   uint16_t* sink = (uint16_t*)e.scratch + lane;  // 128 B: one u16 per lane
   uint32_t* ptab = e.stab;
   const int lo = 1;
   int idx = e.H(H_MT_IDX);
-  int icur = e.S->nf - 1;
-  uint32_t ctr = (uint32_t)uni((int)e.stab[RP_CTR]);
+  int icur = hi;
+  uint32_t ctr = SWAP ? (uint32_t)uni((int)e.stab[RP_CTR]) : 0u;
   // Every chunk reads 64 words. Near the end of the state (idx > 560) the lanes past word 623 compute
   // the next state's first words directly from the current one (new[i] = mix(mt[i], mt[i+1],
   // mt[i+397]) for i < 227, the twist's first phase), so a chunk may run past the end: idx then exceeds
@@ -451,6 +453,9 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
     const int nacc = popc(m);
     const int inext = icur - nacc, idxn = idx + consumed;
 #ifndef MFG_ABLATE_NOSWAP
+    if constexpr (!SWAP) {
+      if (idxn <= 560) yw = mt[idxn + lane];
+    } else {
     // (a chunk with no accepted draw runs the block on the sinks: rare, and one branch less per chunk)
     const bool acc = lanes(m);
     const int i = icur - A, j = (int)r;
@@ -505,6 +510,7 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
     F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
     *pi = (uint16_t)F;
     wave_sync();
+    }
 #else
     if (idxn <= 560) yw = mt[idxn + lane];
 #endif
@@ -515,13 +521,13 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm) {
     mt_twist(e);
     idx -= 624;
   }
-  if (lane == 0) e.stab[RP_CTR] = ctr;
+  if (SWAP && lane == 0) e.stab[RP_CTR] = ctr;
   e.setH(H_MT_IDX, idx);
   wave_sync();
 }
 __device__ __forceinline__ void replay_shuffle(const Env& e, uint16_t* perm) {
-  if (e.S->replay_top14) replay_shuffle_t<true>(e, perm);
-  else replay_shuffle_t<false>(e, perm);
+  if (e.S->replay_top14) replay_shuffle_t<true>(e, perm, e.S->nf - 1);
+  else replay_shuffle_t<false>(e, perm, e.S->nf - 1);
 }
 
 // random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
@@ -1860,7 +1866,9 @@ __device__ void env_reset(const Env& e, int* scratch) {
       m += popc(ballot(em));
     }
     const int j = mt_randbelow_seq<uint16_t>(e, m - 1, m - 1, nullptr);  // first Fisher-Yates step picks the last slot
-    if (m - 2 >= 1) mt_randbelow_seq<uint16_t>(e, m - 2, 1, nullptr);     // remaining draws of shuffle(empty_positions)
+    // (replay_shuffle_t<TOP14, SWAP = false>, the chunked path without swaps, measured slower here: k_resetdone 0.077 ->
+    // 0.091 ms per step at C3)
+    if (m - 2 >= 1) mt_randbelow_seq<uint16_t>(e, m - 2, 1, nullptr);  // remaining draws of shuffle(empty_positions)
     int k = 0, cell = -1;
     const int npos = S->s.n_positions[a];
     if (npos > 0) {
@@ -2928,14 +2936,68 @@ __device__ __forceinline__ void replay_env(SpecP S, uint8_t* slice, uint8_t* rec
   wave_sync();
 }
 
-// Pay every env's pending floor-shuffle debt (once per mfg_step call).
-__global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, uint8_t* state, long long B) {
+// Pay every env's pending floor-shuffle debt (once per mfg_step call). order (optional): the envs in
+// launch order, longest debt first (k_rp_count/k_rp_scan/k_rp_place), so the launch's drain runs short debts.
+__global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, uint8_t* state, long long B,
+                                                         const int* order) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = uni(threadIdx.x >> 6);  // wave-uniform: the slice addresses become scalar
-  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
+  long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
+  if (order) env = uni(order[env]);
   replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
+}
+
+// Replay launch order by debt, longest first (a counting sort over RP_NB debt buckets; envs are
+// independent, so the order changes only which waves are left running at the end of the launch).
+// Order within a bucket is arbitrary. hist: RP_NB ints, zero on entry to k_rp_count.
+#define RP_NB 256
+__global__ void __launch_bounds__(256) k_rp_count(const MfgDevSpec* S_, const uint8_t* state, long long B,
+                                                  int* hist, uint8_t* key) {
+  __shared__ int h[RP_NB];
+  SpecP S = (SpecP)S_;
+  for (int i = threadIdx.x; i < RP_NB; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const long long env = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (env < B) {
+    const int d = ((const int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_DEBT];
+    const int b = RP_NB - 1 - min(max(d, 0), RP_NB - 1);  // bucket 0: the largest debts
+    key[env] = (uint8_t)b;
+    atomicAdd(&h[b], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < RP_NB; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+__global__ void __launch_bounds__(RP_NB) k_rp_scan(int* hist) {  // one block: exclusive scan in place
+  __shared__ int s[RP_NB];
+  const int t = threadIdx.x;
+  const int c = hist[t];
+  s[t] = c;
+  __syncthreads();
+  for (int o = 1; o < RP_NB; o <<= 1) {
+    const int v = t >= o ? s[t - o] : 0;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  hist[t] = s[t] - c;
+}
+__global__ void __launch_bounds__(256) k_rp_place(long long B, int* offs, const uint8_t* key, int* order) {
+  __shared__ int h[RP_NB], base[RP_NB];
+  for (int i = threadIdx.x; i < RP_NB; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const long long env = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int b = 0, r = 0;
+  if (env < B) {
+    b = key[env];
+    r = atomicAdd(&h[b], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < RP_NB; i += blockDim.x) base[i] = h[i] ? atomicAdd(&offs[i], h[i]) : 0;
+  __syncthreads();
+  if (env < B) order[base[b] + r] = (int)env;
 }
 
 // The same for the envs on a step's done list, before k_resetdone resets them: their debt is paid at
@@ -2975,6 +3037,9 @@ struct mfg_engine {
   int rd_slot = 0;     // done list k_logic appends to (alternates per step)
   int rd_blocks = 1;   // k_resetdone workgroups (occupancy x CUs)
   int rpd_blocks = 1;  // k_replay_done workgroups (one wave each)
+  int* rp_hist = nullptr;  // replay order by debt (MFG_REPLAY_LPT): RP_NB bucket counts / offsets
+  int* rp_order = nullptr;  // [B] envs in launch order
+  uint8_t* rp_key = nullptr;  // [B] bucket per env
   hipStream_t ov_stream = nullptr;  // MFG_ABLATE_OVERLAP measurement only (timing of a replay overlapped with the next call)
   hipEvent_t ov_ev = nullptr;
   struct Mark { int k; hipEvent_t a, b; };
@@ -3545,6 +3610,17 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     e->d_bufs.push_back(pool);
     h.pair_pool = (int*)pool;
   }
+  {  // replay launch order (MFG_REPLAY_LPT): debt histogram, per-env bucket, env order
+    void* p = nullptr;
+    const size_t bytes = 4 * (size_t)RP_NB + (size_t)n_envs + 4 * ((size_t)n_envs + 4);
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      delete e; return fail("replay order allocation failed");
+    }
+    e->d_bufs.push_back(p);
+    e->rp_hist = (int*)p;
+    e->rp_order = (int*)p + RP_NB;
+    e->rp_key = (uint8_t*)(e->rp_order + n_envs + 4);
+  }
   {  // auto-reset done lists, both empty
     void* lst = nullptr;
     const size_t bytes = (size_t)2 * 4 * ((size_t)n_envs + 2);
@@ -3731,9 +3807,20 @@ static int replay_impl(mfg_engine* e, void* stream) {
   // K=8 launch against 4 waves per workgroup; MFG_REPLAY_WPB overrides it for measurements)
   static const int rwpb = [] { const char* v = getenv("MFG_REPLAY_WPB"); return v ? atoi(v) : 1; }();
   const int wpb = std::max(1, std::min(rwpb, wpb_for(e->h.lds_replay_per_wave)));
+  // longest debt first (C3: 10.95 -> 10.47 ms per K=8 launch, the order kernels included); MFG_REPLAY_LPT=0 off
+  static const int lpt = [] { const char* v = getenv("MFG_REPLAY_LPT"); return v ? atoi(v) : 1; }();
+  const unsigned g256 = (unsigned)((e->B + 255) / 256);
+  if (lpt) {
+    HIPCHK(hipMemsetAsync(e->rp_hist, 0, 4 * RP_NB, st));
+    hipLaunchKernelGGL(k_rp_count, dim3(g256), dim3(256), 0, st, e->d_spec, e->d_state, (long long)e->B, e->rp_hist,
+                       e->rp_key);
+    hipLaunchKernelGGL(k_rp_scan, dim3(1), dim3(RP_NB), 0, st, e->rp_hist);
+    hipLaunchKernelGGL(k_rp_place, dim3(g256), dim3(256), 0, st, (long long)e->B, e->rp_hist, e->rp_key,
+                       e->rp_order);
+  }
   hipLaunchKernelGGL(k_replay, dim3((unsigned)((e->B + wpb - 1) / wpb)), dim3(wpb * 64),
                      (size_t)e->h.lds_replay_per_wave * wpb, st, e->d_spec, e->d_state,
-                     (long long)e->B);
+                     (long long)e->B, lpt ? (const int*)e->rp_order : nullptr);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
   PROF_END(e, st, MFG_K_REPLAY);
@@ -3743,7 +3830,7 @@ static int replay_impl(mfg_engine* e, void* stream) {
 // K steps. actions: device [K][B][A] int32, or NULL -> Philox4x32-10 synthetic actions keyed
 // (philox_seed, env_base+env) at counter (step_base+k, agent). Outputs (each may be NULL):
 // reward [K][B][A] f64, done [K][B] u8, obs [K][B][A][lmax][d][d], ev_act/ev_watch [K][B][A] u8,
-// ev_misc [K][B][10] i32. auto_reset: envs that finish are reset (the obs row is then the first
+// ev_misc [K][B][MFG_EV_MISC_N] i32. auto_reset: envs that finish are reset (the obs row is then the first
 // observation of the new episode). Per step: k_logic, k_resetdone (auto_reset), k_obs (obs); then one
 // k_replay for the whole call.
 static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
