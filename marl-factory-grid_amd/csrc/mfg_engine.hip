@@ -2682,6 +2682,14 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
 #define MFG_PAIRS_LDS 128    // identifier-collision pairs kept in the k_obs LDS slice
 #define MFG_LDS_MAX 163840  // LDS bytes per CU on gfx950 (one workgroup may use all of it)
 #define MFG_WPB 4  // waves (envs) per workgroup at most; fewer when a slice is large (wpb_for)
+// k_logic<false, false> is SGPR-bound to 7 waves per SIMD (106 SGPRs); asking for 8 fits it in 78 SGPRs with one
+// SGPR spill (C3: 0.1505 -> 0.1303 ms per launch). The same request on the dense k_obs spills ~90 SGPRs into VGPR
+// lanes and made it slower (0.433 -> 0.451 ms), so k_obs keeps 7. MFG_NO_WPE drops the request.
+#ifndef MFG_NO_WPE
+#define MFG_WPE_LOGIC(n) __attribute__((amdgpu_waves_per_eu(n)))
+#else
+#define MFG_WPE_LOGIC(n)
+#endif
 
 // full-record slice: [record][scratch][shuffle tables][BFS scratch if it fits]
 __device__ __forceinline__ void env_full(SpecP S, uint8_t* slice, Env& e, long long env) {
@@ -2761,7 +2769,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, ui
 // One env-step of every env (no reset, no render). FULL: the spec consumes the floor order inside a
 // step (S->step_rng), so the whole record incl. MT/perm is staged; otherwise only the lean prefix.
 template <bool FULL, bool MAINT>
-__global__ void __launch_bounds__(MFG_WPB * 64) k_logic(const MfgDevSpec* S_, uint8_t* state, long long B,
+__global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAINT ? 1 : 8) k_logic(const MfgDevSpec* S_, uint8_t* state, long long B,
                                                         const int32_t* actions, unsigned philox_seed,
                                                         unsigned env_base, long long step, double* reward,
                                                         uint8_t* done, uint8_t* ev_act, uint8_t* ev_watch,
