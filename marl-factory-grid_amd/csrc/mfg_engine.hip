@@ -2969,8 +2969,11 @@ __global__ void __launch_bounds__(256) k_rp_count(const MfgDevSpec* S_, const ui
   __syncthreads();
   const long long env = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (env < B) {
-    const int d = ((const int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_DEBT];
-    const int b = RP_NB - 1 - min(max(d, 0), RP_NB - 1);  // bucket 0: the largest debts
+    const int d = min(max(((const int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_DEBT], 0), 4095);
+    // debts < 64 exact, above that 32 buckets per power of two (C3 K=8 debts are ~100, C5's ~1000)
+    const int lg = 31 - __clz(d | 1);
+    const int q = d < 64 ? d : 64 + (lg - 6) * 32 + ((d >> (lg - 5)) & 31);
+    const int b = RP_NB - 1 - q;  // bucket 0: the largest debts
     key[env] = (uint8_t)b;
     atomicAdd(&h[b], 1);
   }
