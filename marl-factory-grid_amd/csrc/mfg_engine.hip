@@ -2039,16 +2039,24 @@ __device__ void env_reset(const Env& e, int* scratch) {
 // Per-env cell map (one byte per grid cell, in LDS), built once per render and shared by all agents:
 // walls come from the static base map, the dynamic entities are OR-ed in. The ray walk reads its
 // light blockers from it and the placement reads each window cell's tag bits with one LDS load.
-#define CM_WALL 1u     // wall (static)
-#define CM_DOOR 2u     // door present in the global pos_dict
-#define CM_DCLOSED 4u  // ... and closed (blocks light, encodes 0.6666)
-#define CM_ITEM 8u
-#define CM_POD 16u
-#define CM_DROP 32u
-#define CM_DEST 64u    // destination present and not reached
-#define CM_DIRT 128u
+// Bits 0..6 sit at their obs tag's bit (MFG_TAG_*), machines/maintainers one above theirs, so the placement's
+// tag word is a mask and a shift instead of one test per entity kind; the byte map (no machines or
+// maintainers) uses bits 0..7.
+#define CM_WALL 1u       // wall (static)
+#define CM_DOOR 2u       // door present in the global pos_dict
+#define CM_ITEM 4u
+#define CM_POD 8u
+#define CM_DROP 16u
+#define CM_DIRT 32u
+#define CM_DEST 64u      // destination present and not reached
+#define CM_DCLOSED 128u  // door present and closed (blocks light, encodes 0.6666)
 #define CM_MACHINE 256u
 #define CM_MAINT 512u
+static_assert(CM_WALL == 1u << MFG_TAG_WALLS && CM_DOOR == 1u << MFG_TAG_DOORS && CM_ITEM == 1u << MFG_TAG_ITEMS &&
+                  CM_POD == 1u << MFG_TAG_PODS && CM_DROP == 1u << MFG_TAG_DROPOFFS && CM_DIRT == 1u << MFG_TAG_DIRT &&
+                  CM_DEST == 1u << MFG_TAG_DESTS && CM_MACHINE == 2u << MFG_TAG_MACHINES &&
+                  CM_MAINT == 2u << MFG_TAG_MAINTAINERS,
+              "cell-map bits follow the obs tag bits");
 
 __device__ __forceinline__ int v_clamp(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
 template <bool MM>
@@ -2111,17 +2119,14 @@ struct RayLane {
   uint32_t diag;    // bit p: point p is a diagonal step
   __device__ __forceinline__ int dx(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16)) & 0xFF); }
   __device__ __forceinline__ int dy(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16 + 8)) & 0xFF); }
+  static_assert(MAXPTS % 2 == 0 && NW * 4 == 2 * MAXPTS, "a ray's points are whole dwords");
   __device__ __forceinline__ void load(SpecP S, int ray) {
     const bool has = ray < S->nrays;
-    const uint8_t* pts = (const uint8_t*)S->ray_pts + (size_t)(has ? ray : 0) * MAXPTS * 2;
+    // dword loads: a ray's 2 * MAXPTS bytes start on a 4-B boundary (MAXPTS is even, the table is a device
+    // allocation)
+    const uint32_t* pts = (const uint32_t*)S->ray_pts + (size_t)(has ? ray : 0) * NW;
 #pragma unroll
-    for (int q = 0; q < NW; q++) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-        if (4 * q + b < 2 * MAXPTS) w |= (uint32_t)pts[4 * q + b] << (8 * b);
-      pk[q] = w;
-    }
+    for (int q = 0; q < NW; q++) pk[q] = pts[q];
     len = has ? S->ray_len[ray] : 0;
     diag = has ? S->ray_diag[ray] : 0u;
   }
@@ -2319,6 +2324,11 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   const int pA0 = lane < npairs ? pairs.get(lane, 0) : 0, pB0 = lane < npairs ? pairs.get(lane, 1) : 0;
   // agent and ray-origin coordinates: one vector division per render, read per agent with v_readlane
   const int agx = agp / W, agy = agp % W, orgx = org_l / W, orgy = org_l % W;
+  // the first pass's rays are agent independent: loaded once per render, not once per agent, where the
+  // registers they then hold across the agent loop do not cost occupancy (short rays, dense obs)
+  constexpr bool HOIST_RAYS = MAXPTS <= 8 && !PK;
+  RayLane<MAXPTS> ray0;
+  if constexpr (HOIST_RAYS) ray0.load(S, lane);
   for (int a = 0; a < A; a++) {
     const int apos = rl(agp, a);
     const int ax = rl(agx, a), ay = rl(agy, a);
@@ -2343,7 +2353,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     for (int pass = 0; pass < npass; pass++) {
       const int ray_id = pass * MFG_WAVE + lane;
       RayLane<MAXPTS> ray;
-      ray.load(S, ray_id);
+      if (HOIST_RAYS && pass == 0) ray = ray0;
+      else ray.load(S, ray_id);
       // branch-free: every point tests its cell and (from p = 1) both corner cells; the static diagonal
       // mask keeps the corner test only on diagonal steps: cut when both orthogonal neighbours block
       // light (ray_caster.py:89-96)
@@ -2459,16 +2470,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       const uint32_t mraw = cmap_at<MM>(e, cell);
       const uint32_t m = v ? mraw : 0u;
       const bool wall_sup = wsup[inwin ? wi : 0] != 0;
-      uint32_t tags = 0;  // bit t = tag t (< 16) has a (not suppressed) entity here
-      if ((m & CM_WALL) && !wall_sup) tags |= 1u << MFG_TAG_WALLS;
-      if (m & CM_DOOR) tags |= 1u << MFG_TAG_DOORS;
-      if (m & CM_ITEM) tags |= 1u << MFG_TAG_ITEMS;
-      if (m & CM_POD) tags |= 1u << MFG_TAG_PODS;
-      if (m & CM_DROP) tags |= 1u << MFG_TAG_DROPOFFS;
-      if (m & CM_DEST) tags |= 1u << MFG_TAG_DESTS;
-      if (m & CM_DIRT) tags |= 1u << MFG_TAG_DIRT;
-      if (MM && (m & CM_MACHINE)) tags |= 1u << MFG_TAG_MACHINES;
-      if (MM && (m & CM_MAINT)) tags |= 1u << MFG_TAG_MAINTAINERS;
+      // bit t = tag t (< 16) has a (not suppressed) entity here: the cell-map bits are the tag bits
+      uint32_t tags = m & ((wall_sup ? 0u : CM_WALL) | CM_DOOR | CM_ITEM | CM_POD | CM_DROP | CM_DIRT | CM_DEST);
+      if (MM) tags |= (m >> 1) & ((1u << MFG_TAG_MACHINES) | (1u << MFG_TAG_MAINTAINERS));
       // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
       if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
       auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
