@@ -2329,12 +2329,28 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   constexpr bool HOIST_RAYS = MAXPTS <= 8 && !PK;
   RayLane<MAXPTS> ray0;
   if constexpr (HOIST_RAYS) ray0.load(S, lane);
+  // ... and their static light-blocking words are fetched one agent ahead (an L2 round trip behind a
+  // dependent cell_f load, hidden under the previous agent's dedupe and placement)
+  int pf_ofl = -1;
+  uint32_t pf_b = 0, pf_c = 0, pf_d = 0;
+  auto rs_fetch = [&](int ag) {
+    pf_ofl = S->ray_static ? uni((int)S->cell_f[rl(orgx, ag) * W + rl(orgy, ag)]) : -1;
+    if (pf_ofl >= 0) {
+      const bool has = lane < S->nrays;
+      const uint32_t* rs = S->ray_static + ((size_t)pf_ofl * S->nrays + (has ? lane : 0)) * 3;
+      pf_b = has ? rs[0] : 0u;
+      pf_c = has ? rs[1] : 0u;
+      pf_d = has ? rs[2] : 0u;
+    }
+  };
+  if constexpr (HOIST_RAYS) rs_fetch(0);
   for (int a = 0; a < A; a++) {
     const int apos = rl(agp, a);
     const int ax = rl(agx, a), ay = rl(agy, a);
     const int ox = rl(orgx, a), oy = rl(orgy, a);
     const int wx0 = full ? 0 : ax - S->r, wy0 = full ? 0 : ay - S->r;
-    const int ofl = S->ray_static ? uni((int)S->cell_f[ox * W + oy]) : -1;  // origin floor index (static table)
+    // origin floor index (static table)
+    const int ofl = HOIST_RAYS ? pf_ofl : (S->ray_static ? uni((int)S->cell_f[ox * W + oy]) : -1);
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
@@ -2362,11 +2378,19 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       if (ofl >= 0) {
         // the wall part from the per-origin table; only points next to doors are tested here (the door's
         // present/closed state lives in the cell map)
-        const bool has = ray_id < S->nrays;
-        const uint32_t* rs = S->ray_static + ((size_t)ofl * S->nrays + (has ? ray_id : 0)) * 3;
-        blkm = has ? rs[0] : 0u;
-        cutm = has ? rs[1] : 0u;
-        uint32_t dyn = has ? rs[2] : 0u;
+        uint32_t dyn;
+        if (HOIST_RAYS && pass == 0) {
+          blkm = pf_b;
+          cutm = pf_c;
+          dyn = pf_d;
+          if (a + 1 < A) rs_fetch(a + 1);
+        } else {
+          const bool has = ray_id < S->nrays;
+          const uint32_t* rs = S->ray_static + ((size_t)ofl * S->nrays + (has ? ray_id : 0)) * 3;
+          blkm = has ? rs[0] : 0u;
+          cutm = has ? rs[1] : 0u;
+          dyn = has ? rs[2] : 0u;
+        }
         while (dyn) {
           const int p = __ffs((int)dyn) - 1;
           dyn &= dyn - 1;
@@ -2870,7 +2894,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_
 // Observation render of every env into obs[env] (read-only on the state). MM: the spec has machines or
 // maintainers (their tags, identifiers and dedupe); compiled out otherwise to keep the VGPR budget.
 template <int MAXPTS, typename OT, bool MM, bool PK>
-__global__ void __launch_bounds__(MFG_WPB * 64) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
+__global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 && !PK ? 7 : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                       OT* obs, ObsPacked pk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
