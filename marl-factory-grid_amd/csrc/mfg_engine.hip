@@ -2326,7 +2326,12 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   const int agx = agp / W, agy = agp % W, orgx = org_l / W, orgy = org_l % W;
   // the first pass's rays are agent independent: loaded once per render, not once per agent, where the
   // registers they then hold across the agent loop do not cost occupancy (short rays, dense obs)
+#ifdef MFG_NO_RAY_HOIST  // measurement build: rays loaded per agent, ray words still prefetched
+  constexpr bool HOIST_RAYS = false;
+#else
   constexpr bool HOIST_RAYS = MAXPTS <= 8 && !PK;
+#endif
+  constexpr bool PREFETCH_RS = MAXPTS <= 8 && !PK;
   RayLane<MAXPTS> ray0;
   if constexpr (HOIST_RAYS) ray0.load(S, lane);
   // ... and their static light-blocking words are fetched one agent ahead (an L2 round trip behind a
@@ -2343,14 +2348,14 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       pf_d = has ? rs[2] : 0u;
     }
   };
-  if constexpr (HOIST_RAYS) rs_fetch(0);
+  if constexpr (PREFETCH_RS) rs_fetch(0);
   for (int a = 0; a < A; a++) {
     const int apos = rl(agp, a);
     const int ax = rl(agx, a), ay = rl(agy, a);
     const int ox = rl(orgx, a), oy = rl(orgy, a);
     const int wx0 = full ? 0 : ax - S->r, wy0 = full ? 0 : ay - S->r;
     // origin floor index (static table)
-    const int ofl = HOIST_RAYS ? pf_ofl : (S->ray_static ? uni((int)S->cell_f[ox * W + oy]) : -1);
+    const int ofl = PREFETCH_RS ? pf_ofl : (S->ray_static ? uni((int)S->cell_f[ox * W + oy]) : -1);
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
@@ -2379,7 +2384,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         // the wall part from the per-origin table; only points next to doors are tested here (the door's
         // present/closed state lives in the cell map)
         uint32_t dyn;
-        if (HOIST_RAYS && pass == 0) {
+        if (PREFETCH_RS && pass == 0) {
           blkm = pf_b;
           cutm = pf_c;
           dyn = pf_d;
@@ -2491,7 +2496,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
                        ((unsigned)lx < (unsigned)fw) & ((unsigned)ly < (unsigned)fw);
       const bool v = inb & (fv[inb ? lx * fw + ly : 0] != 0xFFFFFFFFu);
       const int cell = v ? x * W + y : 0;
-      const uint32_t mraw = cmap_at<MM>(e, cell);
+      // the cell-map read does not wait for the visibility read: its address is clamped on the bounds alone
+      const uint32_t mraw = cmap_at<MM>(e, inb ? x * W + y : 0);
       const uint32_t m = v ? mraw : 0u;
       const bool wall_sup = wsup[inwin ? wi : 0] != 0;
       // bit t = tag t (< 16) has a (not suppressed) entity here: the cell-map bits are the tag bits
