@@ -2828,15 +2828,8 @@ __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAINT ? 1 
   // (most of the record is per-episode constant: frozen origins, ids, counters of idle rules)
   const bool one_pass = !full && (bytes >> 4) <= MFG_WAVE;
   uint4 orig = make_uint4(0, 0, 0, 0);
-  if (one_pass) {
-    if (e.lane < (bytes >> 4)) {
-      orig = ((const uint4*)rec)[e.lane];
-      ((uint4*)e.lds)[e.lane] = orig;
-    }
-  } else {
-    rec_copy(e.lds, rec, bytes, e.lane);
-  }
-  wave_sync();
+  if (one_pass && e.lane < (bytes >> 4)) orig = ((const uint4*)rec)[e.lane];
+  // the actions (a buffer load or Philox) while the record load is in flight
   const int A = S->A;
   int my_act = 0;
   if (e.lane < A) {
@@ -2847,6 +2840,12 @@ __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAINT ? 1 
       my_act = (int)(((uint64_t)u * (uint64_t)S->s.n_actions[e.lane]) >> 32);
     }
   }
+  if (one_pass) {
+    if (e.lane < (bytes >> 4)) ((uint4*)e.lds)[e.lane] = orig;
+  } else {
+    rec_copy(e.lds, rec, bytes, e.lane);
+  }
+  wave_sync();
   StepOut o;
   env_step<FULL, MAINT>(e, my_act, o, e.scratch);
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
