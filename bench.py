@@ -18,13 +18,20 @@ algorithmic bytes per launch; "pipeline" = the whole step agains
 11,391 B per env-step; "kernels" = every kernel's share. traffic = HBM bytes per launch of the dominant
 kernel from the committed rocprofv3 PMC summary (profiles/pmc_*.json, FETCH_SIZE x2 + WRITE_SIZE).
 cpu_baseline: the C restatement (oracle/, kind "port") on this host's cores, same config and actions,
-bounded sample. Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`,
-one rank per GPU, env ranges sharded (weak scaling), no collective in the data path.
+bounded sample.
+
+Multi-GPU (weak scaling, env ranges sharded, no collective in the data path): either the driver's
+`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`, or plain `python bench.py --gpus N`,
+which starts the N rank processes itself (launch_ranks) before anything touches the GPU and prints rank 0's
+line. Each rank asserts that the RCCL world size equals --gpus (`n_ranks_rccl` in the line).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -61,6 +68,21 @@ def core_bytes(spec):
                abi.RULE_SPAWN_MAINTAINERS):
         const += 2 * spawn(op)
     return 2 * mut + const + A + 8 * A + 1
+
+
+def issue_floors(c, launch_ms):
+    """Issue-unit floors of one launch from its PMC instruction counts (chip totals per dispatch), at 2.4 GHz
+    on 256 CUs: VALU = INSTS_VALU x 2 cycles (a wave64 op on a SIMD-32) over 4 SIMDs per CU; SALU =
+    INSTS_SALU x 1 cycle on the CU's one scalar unit; LDS = SQ_LDS_IDX_ACTIVE (LDS-array cycles, bank-conflict
+    extras included). The binding unit is the largest floor; frac = floor / measured launch time."""
+    cyc = CU_CLOCK_HZ * N_CU
+    floors = {"valu": c['SQ_INSTS_VALU'] * 2 / (4 * cyc) * 1e3, "salu": c['SQ_INSTS_SALU'] / cyc * 1e3}
+    if c.get('SQ_LDS_IDX_ACTIVE') is not None:
+        floors["lds"] = c['SQ_LDS_IDX_ACTIVE'] / cyc * 1e3
+    unit = max(floors, key=floors.get)
+    return {"unit": unit, "frac": round(floors[unit] / launch_ms, 3),
+            "floors_ms": {k: round(v, 4) for k, v in floors.items()},
+            "frac_by_unit": {k: round(v / launch_ms, 3) for k, v in floors.items()}}
 
 
 def algo_bytes(kernel, spec, obs_bytes_per_env, k_launch):
@@ -154,6 +176,127 @@ def load_pmc(workload):
     return None
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, share_gpu=False, dry_run=False):
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed launcher: run N rank processes of this
+    script, one per GPU, and print rank 0's JSON line. The parent stays GPU-free: it only counts devices
+    (torch.cuda.device_count() does not initialise HIP on this image) and starts each rank as a child process
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as torch.distributed.run would.
+    If any rank fails the others are killed (by their own Popen handles) and the largest exit code returned."""
+    if not (share_gpu or dry_run):
+        import torch
+        visible = torch.cuda.device_count()
+        if visible < n:
+            print(f"bench.py: {n} GPUs requested, {visible} visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    out = tempfile.NamedTemporaryFile(prefix='bench_rank0_', suffix='.out', delete=False)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')  # dmabuf IPC only on this pool (RCCL)
+        procs.append(subprocess.Popen([sys.executable, '-u', str(Path(__file__).resolve())] + list(argv), env=env,
+                                      stdout=out if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = max(rc, code if code > 0 else 128 - code)
+                for q in procs:
+                    q.kill()
+                for q in procs:
+                    q.wait()
+                procs = []
+                break
+    out.close()
+    lines = [ln for ln in Path(out.name).read_text().splitlines() if ln.startswith('{')]
+    os.unlink(out.name)
+    if rc == 0 and lines:
+        d = json.loads(lines[-1])
+        d["launcher"] = f"bench.py --gpus {n}: {n} rank processes spawned by a GPU-free parent"
+        print(json.dumps(d), flush=True)
+    elif rc == 0:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
+def init_ranks(args):
+    """(world, rank, local) of this process; joins the process group for world > 1 and checks that the
+    collective backend's world size equals --gpus."""
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if world == 1:
+        return world, rank, local, 1
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    if args.dry_run:
+        dist.init_process_group('gloo')
+    else:
+        if os.environ.get('MFG_BENCH_SHARE_GPU') == '1':  # rehearsal of N ranks on fewer GPUs (not a bench number)
+            local = local % torch.cuda.device_count()
+        torch.cuda.set_device(local)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(args.backend)
+    n_ranks = dist.get_world_size()
+    if n_ranks != world or (args.gpus > 1 and n_ranks != args.gpus):
+        raise SystemExit(f"bench.py: process group has {n_ranks} ranks, expected {world} (--gpus {args.gpus})")
+    return world, rank, local, n_ranks
+
+
+def dry_run(args, world, rank, n_ranks):
+    """CPU rehearsal of the multi-rank protocol (no GPU, gloo): env ranges, barrier-bracketed timed region,
+    MAX over ranks and the metrics all-reduce, with the same output fields as the GPU line."""
+    import torch
+    import torch.distributed as dist
+    from mfg_amd.shard import env_range, allreduce_metrics
+    B = args.batch
+    first, count = env_range(rank, world, B)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    acc = 0
+    for _ in range(args.steps):
+        acc += count
+    elapsed = time.perf_counter() - t0 + 1e-3 * (rank + 1)
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    m = allreduce_metrics(torch.tensor([float(acc)], dtype=torch.float64))
+    ranges = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranges, (first, count))
+    else:
+        ranges = [(first, count)]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "value": B * world * args.steps / elapsed,
+                          "n_gpus": world, "n_ranks_rccl": n_ranks, "steps": args.steps, "max_elapsed_s": elapsed,
+                          "env_ranges": ranges, "metrics_allreduce": float(m[0])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -176,22 +319,19 @@ def main():
     ap.add_argument('--backend', default='nccl', help="torch.distributed backend for N > 1 ('nccl' = RCCL)")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-profile', action='store_true', help='no per-kernel HIP events in the timed region')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='CPU rehearsal of the rank protocol (gloo, no GPU, no engine); not a bench number')
     args = ap.parse_args()
+
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:], share_gpu=os.environ.get('MFG_BENCH_SHARE_GPU') == '1',
+                            dry_run=args.dry_run)
+    world, rank, local, n_ranks = init_ranks(args)
+    if args.dry_run:
+        return dry_run(args, world, rank, n_ranks)
 
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if os.environ.get('MFG_BENCH_SHARE_GPU') == '1':  # rehearsal of N ranks on fewer GPUs (not a bench number)
-        local = local % torch.cuda.device_count()
-    if world > 1:
-        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local)
-        if args.backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-        else:
-            dist.init_process_group(args.backend)
     from mfg_amd.spec import compile_spec
     from mfg_amd.engine import Engine, EV_MISC
     from mfg_amd.shard import env_range
@@ -360,6 +500,7 @@ def main():
                              if c.get('SQ_LDS_IDX_ACTIVE') is not None else None,
                              "lds_bank_conflict_share": round(c['SQ_LDS_BANK_CONFLICT'] / c['SQ_LDS_IDX_ACTIVE'], 3)
                              if c.get('SQ_LDS_IDX_ACTIVE') else None}
+                kd["issue"] = issue_floors(c, kd["mean_launch_ms"])
         step_bytes = core_bytes(spec) + obs_bytes  # C3: 415 + 10,976 = ALGO_BYTES_PER_ENV_STEP
         pipe_bytes = step_bytes * B * k_call
         if dom:
@@ -373,7 +514,11 @@ def main():
                                  "env_steps_per_call": B * k_call, "mean_call_ms": round(mean_call * 1e3, 3),
                                  "achieved": round(pipe_bytes / mean_call / 1e9, 2),
                                  "frac": round(pipe_bytes / mean_call / 1e9 / HBM_PEAK_GBS, 5)},
-                    "kernels": kernels}
+                    "kernels": kernels,
+                    "issue": {k: v["issue"] for k, v in kernels.items() if "issue" in v},
+                    "issue_how": "per kernel: VALU/SALU/LDS-array floors (ms) from the committed PMC pass "
+                                 "(profiles/pmc_*.json) at 2.4 GHz x 256 CUs against this run's launch time; "
+                                 "unit = the binding (largest) floor, frac = floor / launch time"}
         else:
             roof = {"bound": "hbm", "achieved": round(pipe_bytes / mean_call / 1e9, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(pipe_bytes / mean_call / 1e9 / HBM_PEAK_GBS, 5),
@@ -393,13 +538,13 @@ def main():
             v, n, wall = cpu_baseline(args.config, args.cpu_seconds, workers, 12345)
             cpu = {"value": round(v, 1), "unit": "env-steps/s", "cores": workers, "kind": "port",
                    "per_core": round(v / workers, 1),
-                   "all_visible_cores_linear": round(v / workers * visible, 1),
                    "sample": f"{n} env-steps of {args.config} (obs incl., auto-reset) on {workers} processes x "
                              f"{wall:.1f}s, C restatement oracle/mfg_oracle.c, 1 env per process (independent "
                              f"envs: linear in cores); {visible} cores visible, the box allots {BOX_CPU_SHARE} "
                              f"per GPU; {cpu_model()}"}
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+            "n_ranks_rccl": n_ranks,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": f"f64 rewards/battery/dirt, {args.obs_dtype} obs",
@@ -421,4 +566,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main() or 0)

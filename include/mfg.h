@@ -309,10 +309,13 @@ int mfg_layout(const mfg_engine* e, int32_t* out);
 void* mfg_state_ptr(mfg_engine* e);
 int64_t mfg_state_bytes(const mfg_engine* e);
 /* Per-kernel timing (HIP events recorded around every launch on the launch stream while enabled).
- * Kernel ids: MFG_K_LOGIC, MFG_K_RESETDONE, MFG_K_OBS, MFG_K_REPLAY, MFG_K_RESET.
+ * Kernel ids: MFG_K_LOGIC, MFG_K_RESETDONE, MFG_K_OBS, MFG_K_REPLAY, MFG_K_RESET, MFG_K_OBS_DONE (the render of
+ * the envs reset in a step, on the engine's second stream; mfg_step with auto_reset and obs), MFG_K_REPLAY_SEL (the
+ * debt of envs whose RespawnDirt fires in the coming step, paid before k_logic).
  * mfg_profile_read synchronises on the last event, writes total milliseconds and launch counts per
  * kernel id (n entries, up to MFG_K_COUNT) and clears the accumulators. */
-enum { MFG_K_LOGIC = 0, MFG_K_RESETDONE = 1, MFG_K_OBS = 2, MFG_K_REPLAY = 3, MFG_K_RESET = 4, MFG_K_COUNT = 5 };
+enum { MFG_K_LOGIC = 0, MFG_K_RESETDONE = 1, MFG_K_OBS = 2, MFG_K_REPLAY = 3, MFG_K_RESET = 4, MFG_K_OBS_DONE = 5,
+       MFG_K_REPLAY_SEL = 6, MFG_K_COUNT = 7 };
 int mfg_profile(mfg_engine* e, int enable);
 int mfg_profile_read(mfg_engine* e, double* total_ms, int64_t* launches, int n);
 /* Snapshots (checkpoint / resume, parity fixtures): whole state buffer device <-> device. */

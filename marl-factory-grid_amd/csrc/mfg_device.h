@@ -113,6 +113,7 @@ struct MfgDevSpec {
   const uint8_t* base_map8;  // [map_bytes8] the same with u8 cells (specs without machines/maintainers)
   int32_t map_bytes, map_bytes8;  // 2*HW / HW rounded up to 16
   int32_t step_rng;          // a rule consumes the floor order / RNG inside a step (dirt spawns)
+  uint32_t respawn_mask;     // rule indices of RespawnDirt rules (k_replay_sel pays the debt of envs they fire in)
   MfgLayout L;
   int32_t lds_full;          // bytes of dynamic LDS per wave: full record + scratch + shuffle tables
   int32_t lds_logic;         // k_logic: lean record (o_mt bytes) or lds_full when step_rng
@@ -129,6 +130,7 @@ struct MfgDevSpec {
   int32_t pairs_lds;         // pairs held in the k_obs LDS slice; the rest go to pair_pool
   int32_t* pair_pool;        // [B][max_pairs - pairs_lds][3] HBM spill of the pair list, or null
   int32_t* rd_list;          // [2][B + 2]: per step parity, [0] = count, [2..] = envs k_logic flagged done (auto-reset)
+  uint8_t* rd_flag;          // [B]: 1 if k_logic put the env on this step's done list (k_obs leaves it to the list render)
   const int16_t* cell_f;     // [HW] floor index of a cell, -1 for walls
   const uint8_t* node_ok;    // [nf] floor cell has a floor 8-neighbour (a node of points_to_graph)
   int32_t xchg_ordered;      // device applies conflicting ds_wrxchg lanes in lane order (probed at create)

@@ -13,6 +13,23 @@
 #ifndef MFG_OBS_NT
 #define MFG_OBS_NT 1  // k_obs writes the observations with non-temporal stores
 #endif
+// Measurement switches are compile-time only (-D...), never read from the environment at run time:
+//   MFG_NO_RAY_STATIC=1    k_obs tests every ray point against the cell map (no static light table); exact
+//   MFG_REPLAY_EACH_STEP   pay the shuffle debt after every step instead of once per mfg_step call; exact
+//   MFG_ABLATE_*           timing-only ablations, results NOT exact (tools/build_ablation.sh)
+#ifndef MFG_NO_RAY_STATIC
+#define MFG_NO_RAY_STATIC 0
+#endif
+#ifndef MFG_RESET_OVERLAP
+// mfg_step with auto-reset: the resets + their renders on a second stream beside the other envs' render.
+// 0 never, 1 when the reset is long (agents x floor cells >= 16384: the per-agent floor shuffles and draws of
+// SpawnAgents, C4/C5), 2 always
+#define MFG_RESET_OVERLAP 1
+#endif
+#ifndef MFG_RPV
+#define MFG_RPV 3  // k_replay swap-block variant bits (exact; see replay_shuffle_t)
+#endif
+static_assert(!(MFG_RPV & 1) || (MFG_RPV & 2), "MFG_RPV bit 1 (no read sink) needs bit 2 (masked i write)");
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -460,7 +477,11 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     const bool acc = lanes(m);
     const int i = icur - A, j = (int)r;
     uint16_t* const ptop = perm + icur;  // wave-uniform
+#if MFG_RPV & 1  // rejected lanes read the next accepted rank's cell (same address: a broadcast, no sink bank)
+    uint16_t* pi = ptop - A;
+#else
     uint16_t* pi = acc ? ptop - A : sink;
+#endif
     int v = (int)*pi;
     // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
     // the block's own i range (inext, i)), the last one's V_s. Rare at large i: a single scalar test
@@ -505,10 +526,33 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     }
     // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
     // The next chunk's MT words are loaded while the exchange is in flight.
+#if MFG_RPV & 4  // rejected lanes: a no-op (mask 0) on their own rank-table dword instead of a shared u16 sink
+    uint32_t F;
+    {
+      const uint32_t ja = (uint32_t)(uintptr_t)&perm[j];
+      const uint32_t sh = (ja & 2u) << 3;
+      const uint32_t ad = acc ? (ja & ~3u) : (uint32_t)(uintptr_t)&ptab[lane];
+      const uint32_t mk = acc ? 0xFFFFu << sh : 0u, dt = acc ? (uint32_t)v << sh : 0u;
+      asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(F) : "v"(ad), "v"(mk), "v"(dt) : "memory");
+      if (idxn <= 560) yw = mt[idxn + lane];
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F) : : "memory");
+      F = (F >> sh) & 0xFFFFu;
+    }
+#elif MFG_RPV & 8  // rejected lanes exec-masked out of the exchange
+    uint32_t F = 0;
+    if (acc) F = lds_xchg_u16_issue(&perm[j], (uint32_t)v);
+    if (idxn <= 560) yw = mt[idxn + lane];
+    F = lds_xchg_u16_wait(F, &perm[j]);
+#else
     uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
     if (idxn <= 560) yw = mt[idxn + lane];
     F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
+#endif
+#if MFG_RPV & 2  // only accepted lanes write their i cell (exec mask) instead of rejected lanes writing a sink
+    if (acc) *pi = (uint16_t)F;
+#else
     *pi = (uint16_t)F;
+#endif
     wave_sync();
     }
 #else
@@ -2281,7 +2325,7 @@ struct ObsPacked {
   int cap, E;
 };
 
-template <int MAXPTS, typename OT, bool MM, bool PK>
+template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
 __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPacked& pk) {
   SpecP S = e.S;
   // window: oh x ow cells from (wx0, wy0) = agent - r, or the whole level at (0, 0) when pomdp_r == 0
@@ -2316,6 +2360,12 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   const int ndsup = S->dirt_cap >> 5;
   // agents on each window cell: [dd][2] u32 (bit b = agent b), filled by a lane-per-agent scatter
   lds_u32* amw = dsup + ndsup;
+  // window dirt map (specs with dirt): per window cell 1 + the index of the last present, non-suppressed pile on
+  // it, built per agent from the pile table (lane = pile), so the placement reads a cell's pile instead of
+  // scanning every pile per 64-cell block (C5: up to 384 piles)
+  lds_u32* wdirt = amw + 2 * dd;
+  constexpr bool has_dirt = DIRT;  // S->dirt_cap != 0 (a template parameter: the register budget of k_obs)
+  const float invW = 1.0f / (float)W;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
   const int agp = lane < A ? e.agpos()[lane] : -1;
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
@@ -2360,6 +2410,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
     for (int i = lane; i < 2 * dd; i += MFG_WAVE) amw[i] = 0u;
+    if (has_dirt)
+      for (int i = lane; i < dd; i += MFG_WAVE) wdirt[i] = 0u;
     wave_sync();
     if (lane < A) {  // scatter the agents into the window's agent masks
       const int wx = agx - wx0, wy = agy - wy0;
@@ -2467,6 +2519,21 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       }
     }
     wave_sync();
+    if (has_dirt) {
+      // clean_up piles on window cells, in table order: the last one wins (the sequential scan it replaces
+      // kept the last matching pile's amount); cell / W through a float reciprocal (exact for cells < 2^16)
+      for (int b = 0; b < nT; b += MFG_WAVE) {
+        const int i = b + lane;
+        const int w = i < nT ? e.dirtpos()[i] : 0;
+        const int c = EW_POS(w);
+        const int cx = (int)(((float)c + 0.5f) * invW), cy = c - cx * W;
+        const int px = cx - wx0, py = cy - wy0;
+        if (i < nT && (w & EW_PRESENT) && c != EW_NOPOS && (unsigned)px < (unsigned)oh && (unsigned)py < (unsigned)ow &&
+            !sup.dirt_sup(i))
+          atomicMax((uint32_t*)&wdirt[px * ow + py], (uint32_t)(i + 1));
+      }
+      wave_sync();
+    }
     OT* out_a = PK ? nullptr : out_env + (size_t)a * S->obs_agent_stride;
     const int nl = S->s.n_layers[a];
     // packed mode: entry count so far and the projection accumulators (lane j holds outputs j, 64 + j, ...)
@@ -2521,14 +2588,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       if (MM && S->mmax) resup(e.machines(), e.H(H_N_MACHINES), sup.machines, MFG_TAG_MACHINES, false);
       if (MM && S->kmax) resup(e.maints(), e.H(H_N_MAINTS), sup.maints, MFG_TAG_MAINTAINERS, false);
       double dirt_amt = 0.0;
-      if (ballot(m & CM_DIRT)) {  // amount of the (last non-suppressed) pile on the cell
-        bool any = false;
-        for (int i = 0; i < nT; i++) {
-          const int w = uni(e.dirtpos()[i]);
-          const double am = e.dirtamt()[i];
-          if (v && EW_POS(w) == cell && (w & EW_PRESENT) && !sup.dirt_sup(i)) { any = true; dirt_amt = am; }
-        }
-        tags = any ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
+      if (has_dirt) {  // amount of the last non-suppressed pile on the cell (window dirt map)
+        const uint32_t di = v ? wdirt[inwin ? wi : 0] : 0u;
+        dirt_amt = di ? e.dirtamt()[di - 1] : 0.0;
+        tags = di ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
       }
       const int wic = inwin ? wi : 0;
       const u64 amraw = (u64)amw[2 * wic] | ((u64)amw[2 * wic + 1] << 32);
@@ -2849,6 +2912,7 @@ __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAINT ? 1 
   StepOut o;
   env_step<FULL, MAINT>(e, my_act, o, e.scratch);
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
+  if (e.lane == 0) S->rd_flag[env] = (o.done && auto_reset) ? 1 : 0;
   if (o.done && auto_reset) {
     e.setH(H_DONE, 1);
     // append to this step's done list (k_resetdone walks it instead of one wave per env)
@@ -2898,16 +2962,11 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_
 
 // Observation render of every env into obs[env] (read-only on the state). MM: the spec has machines or
 // maintainers (their tags, identifiers and dedupe); compiled out otherwise to keep the VGPR budget.
-template <int MAXPTS, typename OT, bool MM, bool PK>
-__global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 && !PK ? 7 : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
-                                                      OT* obs, ObsPacked pk) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  SpecP S = (SpecP)S_;
-  const int wid = uni(threadIdx.x >> 6);  // wave-uniform: slice and record addresses become scalar
-  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
-  if (env >= B) return;
+// One env's render (observation_builder.py:138-235) in its LDS slice.
+template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
+__device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* state, long long env, OT* obs,
+                                        ObsPacked pk) {
   // slice: [lean record][cell map][pairs]
-  uint8_t* slice = smem + (size_t)wid * S->lds_obs;
   Env e;
   e.S = S; e.lds = slice; e.stab = nullptr;
   e.cmap = slice + S->L.o_mt;
@@ -2924,11 +2983,40 @@ __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_
     pk.val = pk.val ? pk.val + ea * pk.cap : nullptr;
     pk.cnt = pk.cnt ? pk.cnt + ea : nullptr;
     pk.emb = pk.emb ? pk.emb + ea * pk.E : nullptr;
-    build_obs<MAXPTS, OT, MM, PK>(e, nullptr, pg, pk);
+    build_obs<MAXPTS, OT, MM, PK, DIRT>(e, nullptr, pg, pk);
   } else {
-    build_obs<MAXPTS, OT, MM, PK>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg, pk);
+    build_obs<MAXPTS, OT, MM, PK, DIRT>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg, pk);
   }
   if (e.lane == 0 && e.hdrp[H_OVERFLOW]) ((int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_OVERFLOW] = 1;
+}
+
+// Render of every env (skip: envs k_logic put on this step's done list, rendered by k_obs_list after their reset
+// on the engine's second stream; null = none). With auto-reset, mfg_step renders the envs that did not finish
+// on the caller's stream while the finished ones are reset and rendered beside it.
+template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
+__global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 && !PK ? 7 : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
+                                                      OT* obs, ObsPacked pk, const uint8_t* skip) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const int wid = uni(threadIdx.x >> 6);  // wave-uniform: slice and record addresses become scalar
+  const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
+  if (env >= B) return;
+  if (skip && skip[env]) return;
+  obs_env<MAXPTS, OT, MM, PK, DIRT>(S, smem + (size_t)wid * S->lds_obs, state, env, obs, pk);
+}
+// Render of the envs of a done list (rd_list row: [0] = count, [2..] = envs): a resident grid strides over it.
+template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
+__global__ void __launch_bounds__(MFG_WPB * 64) k_obs_list(const MfgDevSpec* S_, const uint8_t* state, long long B,
+                                                           OT* obs, ObsPacked pk, const int32_t* list) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const int wid = uni(threadIdx.x >> 6);
+  const long long n = min((long long)uni(list[0]), B);
+  const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+  for (long long q = (long long)blockIdx.x * (blockDim.x >> 6) + wid; q < n; q += nw) {
+    const long long env = uni(list[2 + q]);
+    if (env >= 0 && env < B) obs_env<MAXPTS, OT, MM, PK, DIRT>(S, smem + (size_t)wid * S->lds_obs, state, env, obs, pk);
+  }
 }
 
 // Pay one env's pending floor-shuffle debt in a k_replay-sized LDS slice. Touches only the header, MT state
@@ -2988,6 +3076,22 @@ __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec* S_, u
   if (env >= B) return;
   if (order) env = uni(order[env]);
   replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
+}
+
+// The debt of the envs whose RespawnDirt rule fires in the coming step (its counter is 0: clean_up/rules.py:49-59
+// spawns from the floor order), paid at k_replay's occupancy before k_logic<FULL> reaches the spawn; k_logic then
+// pays inline only the debt of that step's own moves (C4: ~1/16 of the envs per step carry up to K steps of debt).
+__global__ void __launch_bounds__(64) k_replay_sel(const MfgDevSpec* S_, uint8_t* state, long long B) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const long long env = blockIdx.x;
+  if (env >= B) return;
+  uint8_t* rec = state + (size_t)env * S->L.size;
+  const int* rc = (const int*)(rec + S->L.o_rule_ctr);
+  bool fire = false;
+  for (uint32_t m = S->respawn_mask; m; m &= m - 1) fire |= uni(rc[__ffs(m) - 1]) == 0;
+  if (!fire) return;
+  replay_env(S, smem, rec);
 }
 
 // Replay launch order by debt, longest first (a counting sort over RP_NB debt buckets; envs are
@@ -3084,6 +3188,10 @@ struct mfg_engine {
   int* rp_hist = nullptr;  // replay order by debt (MFG_REPLAY_LPT): RP_NB bucket counts / offsets
   int* rp_order = nullptr;  // [B] envs in launch order
   uint8_t* rp_key = nullptr;  // [B] bucket per env
+  hipStream_t aux = nullptr;  // second stream: resets of a step's done envs and their render (MFG_RESET_OVERLAP)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int obs_list_blocks = 1;  // workgroups of the done-list render (resident grid, strides over the list)
+  bool overlap = false;     // resets beside the render (MFG_RESET_OVERLAP)
   hipStream_t ov_stream = nullptr;  // MFG_ABLATE_OVERLAP measurement only (timing of a replay overlapped with the next call)
   hipEvent_t ov_ev = nullptr;
   struct Mark { int k; hipEvent_t a, b; };
@@ -3481,6 +3589,9 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   h.step_rng = 0;
   for (int r = 0; r < s->n_rules; r++)  // dirt spawns and maintainer retargets consume the floor order mid-step
     if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT || s->rules[r].op == MFG_RULE_MOVE_MAINTAINERS) h.step_rng = 1;
+  h.respawn_mask = 0;
+  for (int r = 0; r < s->n_rules && r < 32; r++)
+    if (s->rules[r].op == MFG_RULE_RESPAWN_DIRT) h.respawn_mask |= 1u << r;
   h.map_bytes = align_up(2 * HW, 16);
   h.map_bytes8 = align_up(HW, 16);
   h.lds_full = align_up(h.L.size + h.scratch_bytes + 4 * MFG_STAB_N, 16);
@@ -3506,7 +3617,8 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   h.fv_words = align_up((2 * h.fr + 1) * (2 * h.fr + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
-              8 * h.dd;  // + per-window-cell agent masks (u64)
+              8 * h.dd +  // + per-window-cell agent masks (u64)
+              (h.dirt_cap ? 4 * h.dd : 0);  // + window dirt map
   // replay kernel slice: [hdr 32 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = probe_xchg_order(device);
@@ -3585,7 +3697,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   {  // static light-blocking table per (origin floor cell, ray): walls only; door-dependent points flagged
     const size_t n = (size_t)s->n_floor * h.nrays * 3;
     h.ray_static = nullptr;
-    if (n * 4 <= ((size_t)256 << 20) && !getenv("MFG_NO_RAY_STATIC")) {
+    if (n * 4 <= ((size_t)256 << 20) && !MFG_NO_RAY_STATIC) {
       std::vector<uint32_t> rs(n, 0u);
       auto wall = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && s->level[x * s->W + y] == 1; };
       auto door = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && door_of[x * s->W + y] != 0xFF; };
@@ -3674,6 +3786,20 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     }
     e->d_bufs.push_back(lst);
     h.rd_list = (int32_t*)lst;
+    void* fl = nullptr;
+    if (hipMalloc(&fl, (size_t)n_envs) != hipSuccess || hipMemset(fl, 0, (size_t)n_envs) != hipSuccess) {
+      if (fl) (void)hipFree(fl);
+      delete e; return fail("done flag allocation failed");
+    }
+    e->d_bufs.push_back(fl);
+    h.rd_flag = (uint8_t*)fl;
+  }
+  int prio_lo = 0, prio_hi = 0;  // the resets' stream first: their waves are a long serial chain each
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&e->aux, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
+    delete e; return fail("stream/event creation failed");
   }
   if (h.bfs_bytes && !h.bfs_off) {  // BFS scratch in HBM, one slice per env
     void* pool = nullptr;
@@ -3701,6 +3827,10 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
       delete e; return fail("occupancy query failed");
     }
     e->rpd_blocks = std::max(1, per_cu) * std::max(1, n_cu);
+    e->overlap = MFG_RESET_OVERLAP == 2 || (MFG_RESET_OVERLAP == 1 && (long long)h.A * h.nf >= 16384);
+    const int ow = std::min(MFG_WPB, wpb_for(h.lds_obs));
+    const int obs_per_cu = std::max(1, std::min(32 / ow, (int)(MFG_LDS_MAX / ((size_t)h.lds_obs * ow))));
+    e->obs_list_blocks = obs_per_cu * std::max(1, n_cu);
   }
   *out = e;
   return 0;
@@ -3714,6 +3844,12 @@ extern "C" int mfg_destroy(mfg_engine* e) {
   if (e->d_state) (void)hipFree(e->d_state);
   for (auto& m : e->marks) { e->ev_free.push_back(m.a); e->ev_free.push_back(m.b); }
   for (hipEvent_t ev : e->ev_free) (void)hipEventDestroy(ev);
+  if (e->aux) (void)hipStreamSynchronize(e->aux);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->aux) (void)hipStreamDestroy(e->aux);
+  if (e->ov_stream) (void)hipStreamDestroy(e->ov_stream);
+  if (e->ov_ev) (void)hipEventDestroy(e->ov_ev);
   delete e;
   return 0;
 }
@@ -3748,14 +3884,30 @@ static const int obs_wpb = wpb_env("MFG_OBS_WPB", MFG_WPB), logic_wpb = wpb_env(
 #define GEOMW(lds, W) dim3(env_grid(e, std::min(W, wpb_for(lds)))), dim3(std::min(W, wpb_for(lds)) * 64), \
     (size_t)(lds) * std::min(W, wpb_for(lds))
 
+// k_obs over every env (list = null; skip: flags of envs left to a list render) or over a done list (a resident
+// grid striding over it)
 template <int MP, typename OT, bool PK>
-static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipStream_t st) {
-  if (e->h.mmax || e->h.kmax)
-    hipLaunchKernelGGL((k_obs<MP, OT, true, PK>), GEOMW(e->h.lds_obs, obs_wpb),
-                       st, e->d_spec, e->d_state, (long long)e->B, obs, pk);
-  else
-    hipLaunchKernelGGL((k_obs<MP, OT, false, PK>), GEOMW(e->h.lds_obs, obs_wpb),
-                       st, e->d_spec, e->d_state, (long long)e->B, obs, pk);
+static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipStream_t st, const uint8_t* skip,
+                               const int32_t* list) {
+  const int W = std::min(obs_wpb, wpb_for(e->h.lds_obs));
+  const unsigned grid = list ? (unsigned)std::min<long long>(env_grid(e, W), e->obs_list_blocks) : env_grid(e, W);
+  const size_t lds = (size_t)e->h.lds_obs * W;
+  const long long B = e->B;
+  const bool mm = e->h.mmax || e->h.kmax, dirt = e->h.dirt_cap != 0;
+#define OBS_LAUNCH(MMV, DV)                                                                                     \
+  do {                                                                                                          \
+    if (list)                                                                                                   \
+      hipLaunchKernelGGL((k_obs_list<MP, OT, MMV, PK, DV>), dim3(grid), dim3(W * 64), lds, st, e->d_spec,     \
+                         e->d_state, B, obs, pk, list);                                                         \
+    else                                                                                                        \
+      hipLaunchKernelGGL((k_obs<MP, OT, MMV, PK, DV>), dim3(grid), dim3(W * 64), lds, st, e->d_spec, e->d_state, \
+                         B, obs, pk, skip);                                                                     \
+  } while (0)
+  if (mm && dirt) OBS_LAUNCH(true, true);
+  else if (mm) OBS_LAUNCH(true, false);
+  else if (dirt) OBS_LAUNCH(false, true);
+  else OBS_LAUNCH(false, false);
+#undef OBS_LAUNCH
   return hipGetLastError();
 }
 
@@ -3800,20 +3952,21 @@ static ObsPacked packed_rows(const mfg_engine* e, const mfg_packed_obs* p, int k
 }
 
 // render obs of every env into obs (obs_dtype 0 = f32, 1 = f64, 2 = packed: obs -> mfg_packed_obs, row k)
-static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st, int k = 0) {
+static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st, int k = 0,
+                      const uint8_t* skip = nullptr, const int32_t* list = nullptr, int kid = MFG_K_OBS) {
   hipError_t err = hipSuccess;
   PROF_BEGIN(e, st);
   ObsPacked none{};
   if (obs_dtype == MFG_OBS_PACKED) {
     const ObsPacked pk = packed_rows(e, (const mfg_packed_obs*)obs, k);
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, true>(e, (float*)nullptr, pk, st)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, true>(e, (float*)nullptr, pk, st, skip, list)));
   } else if (obs_dtype == MFG_OBS_F64) {
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double, false>(e, (double*)obs, none, st)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double, false>(e, (double*)obs, none, st, skip, list)));
   } else {
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, false>(e, (float*)obs, none, st)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, false>(e, (float*)obs, none, st, skip, list)));
   }
   if (err != hipSuccess) return fail(std::string("k_obs launch: ") + hipGetErrorString(err));
-  PROF_END(e, st, MFG_K_OBS);
+  PROF_END(e, st, kid);
   return 0;
 }
 
@@ -3898,6 +4051,14 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
   const size_t obs_row = B * A * (size_t)e->h.obs_agent_stride * (obs_dtype == MFG_OBS_F64 ? 8 : 4);
   for (int k = 0; k < K; k++) {
     const size_t kb = (size_t)k * B;
+    if (e->h.respawn_mask) {
+      PROF_BEGIN(e, st);
+      hipLaunchKernelGGL(k_replay_sel, dim3((unsigned)e->B), dim3(64), (size_t)e->h.lds_replay_per_wave, st, e->d_spec,
+                         e->d_state, (long long)e->B);
+      hipError_t err = hipGetLastError();
+      if (err != hipSuccess) return fail(std::string("k_replay_sel launch: ") + hipGetErrorString(err));
+      PROF_END(e, st, MFG_K_REPLAY_SEL);
+    }
     {
     PROF_BEGIN(e, st);
     if (e->h.bfs_bytes) {
@@ -3928,33 +4089,50 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     }
     const int rd_cur = e->rd_slot;
     e->rd_slot ^= 1;  // the next k_logic appends to the other list (and empties this one after k_resetdone)
-    // measurement switch: pay the debt every step (before the resets) instead of once per call
-    static const int replay_each = [] { const char* v = getenv("MFG_REPLAY_EACH_STEP"); return v ? atoi(v) : 0; }();
-    if (replay_each && k + 1 < K && replay_impl(e, stream)) return -1;
+#ifdef MFG_REPLAY_EACH_STEP  // measurement build (exact): pay the debt every step instead of once per call
+    if (k + 1 < K && replay_impl(e, stream)) return -1;
+#endif
+    void* obs_k = obs && obs_dtype != MFG_OBS_PACKED ? (void*)((uint8_t*)obs + (size_t)k * obs_row) : obs;
+#ifdef MFG_ABLATE_NOOBS
+    obs_k = nullptr;
+#endif
+    // With auto-reset and obs, the done envs are reset and rendered on the engine's second stream while the
+    // caller's stream renders every other env (k_logic's rd_flag tells k_obs which to leave out): a step's
+    // resets are a few hundred latency-bound waves (C4: ~2.4 ms) that the full render hides.
+    const bool split = e->overlap && auto_reset && obs_k;
+    hipStream_t rs = split ? e->aux : st;
+    if (split) {
+      HIPCHK(hipEventRecord(e->ev_fork, st));
+      HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
+    }
     if (auto_reset) {
-      PROF_BEGIN(e, st);
+      PROF_BEGIN(e, rs);
       // the done envs' debt first, at k_replay's occupancy; k_resetdone then finds none left to pay
       hipLaunchKernelGGL(k_replay_done, dim3((unsigned)std::min<long long>(e->B, e->rpd_blocks)), dim3(64),
-                         (size_t)e->h.lds_replay_per_wave, st, e->d_spec, e->d_state, (long long)e->B, rd_cur);
+                         (size_t)e->h.lds_replay_per_wave, rs, e->d_spec, e->d_state, (long long)e->B, rd_cur);
       const int wpb = wpb_for(e->h.lds_full);
       const long long nwg = std::min<long long>(env_grid(e, wpb), e->rd_blocks);
-      hipLaunchKernelGGL(k_resetdone, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, st,
+      hipLaunchKernelGGL(k_resetdone, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, rs,
                          e->d_spec, e->d_state, (long long)e->B, rd_cur);
       hipError_t err = hipGetLastError();
       if (err != hipSuccess) return fail(std::string("k_resetdone launch: ") + hipGetErrorString(err));
-      PROF_END(e, st, MFG_K_RESETDONE);
+      PROF_END(e, rs, MFG_K_RESETDONE);
     }
-#ifndef MFG_ABLATE_NOOBS
-    if (obs && obs_dtype == MFG_OBS_PACKED && launch_obs(e, obs, obs_dtype, st, k)) return -1;
-    if (obs && obs_dtype != MFG_OBS_PACKED && launch_obs(e, (uint8_t*)obs + (size_t)k * obs_row, obs_dtype, st))
+    if (split) {
+      const int32_t* lst = e->h.rd_list + (size_t)rd_cur * (size_t)(e->B + 2);
+      if (launch_obs(e, obs_k, obs_dtype, rs, k, nullptr, lst, MFG_K_OBS_DONE)) return -1;
+      if (launch_obs(e, obs_k, obs_dtype, st, k, e->h.rd_flag, nullptr, MFG_K_OBS)) return -1;
+      HIPCHK(hipEventRecord(e->ev_join, rs));
+      HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
+    } else if (obs_k && launch_obs(e, obs_k, obs_dtype, st, k)) {
       return -1;
-#endif
+    }
   }
-  // measurement switch (results NOT exact: the replay races the next call's k_logic header write-back and
+#ifdef MFG_ABLATE_OVERLAP
+  // timing-only build (results NOT exact: the replay races the next call's k_logic header write-back and
   // k_resetdone; run with auto_reset = 0): the call's replay runs on a second stream, overlapped with the
-  // next call's kernels, to price a pipelined replay
-  static const int overlap = [] { const char* v = getenv("MFG_ABLATE_OVERLAP"); return v ? atoi(v) : 0; }();
-  if (overlap) {
+  // next call's kernels, to price a pipelined replay. Never part of the product library.
+  {
     if (!e->ov_stream) {
       HIPCHK(hipStreamCreateWithFlags(&e->ov_stream, hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&e->ov_ev, hipEventDisableTiming));
@@ -3963,6 +4141,7 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     HIPCHK(hipStreamWaitEvent(e->ov_stream, e->ov_ev, 0));
     return replay_impl(e, e->ov_stream);
   }
+#endif
   return replay_impl(e, stream);
 }
 
@@ -3991,7 +4170,7 @@ extern "C" int mfg_profile_read(mfg_engine* e, double* total_ms, int64_t* launch
 static int profile_read_impl(mfg_engine* e, double* total_ms, int64_t* launches, int n) {
   if (!total_ms || !launches) return fail("null argument");
   for (int k = 0; k < n; k++) { total_ms[k] = 0.0; launches[k] = 0; }
-  if (!e->marks.empty()) HIPCHK(hipEventSynchronize(e->marks.back().b));
+  for (const auto& m : e->marks) HIPCHK(hipEventSynchronize(m.b));  // marks may sit on both streams
   for (const auto& m : e->marks) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, m.a, m.b));

@@ -15,7 +15,7 @@ from . import abi
 LIB_PATH = Path(os.environ.get('MFG_HIP_LIB') or Path(__file__).resolve().parent / '_lib' / 'libmfg_hip.so')
 EV_MISC = abi.EV_MISC_N  # MFG_EV_MISC_N (include/mfg.h)
 HDR_N = 40  # MFG_HDR_N (csrc/mfg_device.h)
-KERNELS = ['k_logic', 'k_resetdone', 'k_obs', 'k_replay', 'k_reset']  # MFG_K_* ids (include/mfg.h)
+KERNELS = ['k_logic', 'k_resetdone', 'k_obs', 'k_replay', 'k_reset', 'k_obs_done', 'k_replay_sel']  # MFG_K_* ids (include/mfg.h)
 
 LAYOUT_KEYS = ['size', 'o_hdr', 'o_rule_ctr', 'o_agent_pos', 'o_agent_arr', 'o_agent_par', 'o_frozen_org',
                'o_frozen_gp', 'o_door', 'o_items', 'o_pods', 'o_drops', 'o_dests', 'o_dirt_pos', 'o_dirt_id',

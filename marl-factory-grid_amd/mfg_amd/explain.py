@@ -48,10 +48,45 @@ _ENTITY_KWARGS = {
 }
 
 
+def _custom_rules(folder):
+    """{name: {kwarg: default or '!'}} of the Rule subclasses defined under `folder` (tools.py:43-58 explains a
+    class by its and its bases' __init__ signatures). Custom Rules are the custom plugin kind this build runs
+    (on the host, mfg_amd.host_rules); custom Actions and Entities are rejected by compile_spec."""
+    import importlib.util
+    import inspect
+    import sys
+    folder = Path(folder).resolve()
+    out = {}
+    for path in sorted(folder.rglob('*.py')):
+        if '__init__' in path.name:
+            continue
+        mod_name = 'mfg_custom_' + '_'.join(path.relative_to(folder).with_suffix('').parts)
+        mod = sys.modules.get(mod_name)
+        if mod is None:
+            spec = importlib.util.spec_from_file_location(mod_name, path)
+            mod = importlib.util.module_from_spec(spec)
+            sys.modules[mod_name] = mod
+            spec.loader.exec_module(mod)
+        for key, obj in vars(mod).items():
+            if key.startswith('_') or not inspect.isclass(obj) or obj.__module__ != mod_name:
+                continue
+            if not any(b.__name__ == 'Rule' for b in obj.__mro__[1:]):
+                continue
+            params = {}
+            for cls in reversed(obj.__mro__[:-1]):
+                try:
+                    params.update(inspect.signature(cls).parameters)
+                except (TypeError, ValueError):
+                    pass
+            out[key] = {k: (v.default if v.default is not inspect.Parameter.empty else '!')
+                        for k, v in params.items() if k not in ('self', 'args', 'kwargs')}
+    return out
+
+
 class ConfigExplainer:
     def __init__(self, custom_path=None):
-        if custom_path is not None:
-            raise NotImplementedError('custom modules run outside the engine (see mfg_amd.plugins)')
+        # utils/tools.py:24-39: with a custom path, its modules' classes are explained beside the built-ins
+        self.custom_path = Path(custom_path) if custom_path is not None else None
 
     def get_actions(self):
         acts = {k: {'valid_reward': v[3], 'fail_reward': v[4]} for k, v in _spec._ACTIONS.items()}
@@ -72,7 +107,11 @@ class ConfigExplainer:
                                            'Positions': ['(x, y)'], 'Clones': 0, 'is_blocking_pos': False}}}
 
     def get_rules(self):
-        return {k: dict(v) for k, v in _RULE_KWARGS.items()}
+        out = {k: dict(v) for k, v in _RULE_KWARGS.items()}
+        if self.custom_path is not None:
+            for k, v in _custom_rules(self.custom_path).items():
+                out.setdefault(k, v)  # a built-in name wins, as in the rule loader (config_parser.py:213-233)
+        return out
 
     def get_observations(self):
         return sorted(set(list(_spec._POS_TAGS) + ['Self', 'Other', 'Agent', 'Combined', 'Placeholder', 'Battery',

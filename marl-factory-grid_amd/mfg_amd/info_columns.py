@@ -45,6 +45,17 @@ class InfoColumns:
                 slots = [j for j, ac in enumerate(spec.agent_actions[a]) if ac['cls'] == cls]
                 self._ops.append((key(f'{n}_{cls}'), 'action', (a, slots)))
             self._ops.append((key(f'{n}_Collisions'), 'act_coll', (a,)))
+        # destination slots of one env (the engine's destmax, mfg_create): bounds the per-step reach count, so the
+        # exact one-add-per-destination fold needs no device->host read of the count
+        self._dest_max = 0
+        for op, ri_, _ in spec.rules:
+            if op == abi.RULE_SPAWN_DESTS:
+                self._dest_max = int(ri_[0])
+            elif op == abi.RULE_SPAWN_DEST_ON_AGENT:
+                self._dest_max = spec.n_agents
+            elif op == abi.RULE_SPAWN_DEST_PER_AGENT:
+                self._dest_max = int(spec.c.n_dest_entries)
+        self._dest_max = min(self._dest_max, 31)  # the 5-bit reach counter of ev_watch
         # 2) tick_step results in rule order
         dest_seen = False
         for ri, (op, ri_, rf) in enumerate(spec.rules):
@@ -156,7 +167,7 @@ class InfoColumns:
             elif kind == 'dest_reach':
                 a, r = p
                 n = (watch[:, a] >> 3) & 31
-                for c in range(int(n.max().item()) if B else 0):  # one addition per credited destination
+                for c in range(self._dest_max):  # one addition per credited destination (no host sync)
                     add(k, n > c, r)
             elif kind == 'respawn_items':
                 v = misc[:, abi.EVM_RESPAWN_ITEMS]

@@ -203,6 +203,12 @@ class BatchedA2C:
             raise ValueError('BatchedA2C shares one network: all agents need the same number of actions')
         self.n_actions = n_act.pop()
         kdim = eng.lmax * eng.obs_hw[0] * eng.obs_hw[1]
+        if not check_cap and cap < kdim:
+            # a truncated row would make acting (the fused emb sums every nonzero entry) and learning (the stored
+            # cap entries only) see different obs_proj inputs: skipping the check is allowed only when no row
+            # can be truncated
+            raise ValueError(f'check_cap=False needs cap >= lmax*h*w = {kdim} (rows can hold up to that many '
+                             f'nonzero entries); got cap {cap}')
         self.net = net if net is not None else RecurrentAC(
             kdim, self.n_actions, obs_emb_size, action_emb_size, hidden_size, hidden_size, self.A,
             use_agent_embedding=use_agent_embedding)

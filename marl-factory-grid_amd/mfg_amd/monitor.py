@@ -3,11 +3,17 @@
 * `EnvMonitor` -- utils/logging/envmonitor.py:14-73: wraps a `Factory`, keeps every step's info dict
   and, at each done, aggregates the episode (columns ending in 'ount' averaged, the others summed,
   IGNORED_DF_COLUMNS dropped, helpers.py:26-28) into one DataFrame row; `save_monitor` pickles the
-  DataFrame (our own file, written the way the reference writes it). Plotting is not part of this build.
+  DataFrame (our own file, written the way the reference writes it); `auto_plotting_keys` plots the saved
+  file with `mfg_amd.plotting.plot_single_run` (utils/plotting/plot_single_runs.py).
 * `EnvRecorder` -- utils/logging/recorder.py:10-190: records `summarize_state()` per step for the chosen
   episodes and writes them with the reference's record layout ({'episodes': [{'steps', 'episode_nr'}],
   'n_episodes', 'metadata', 'header'}). The reference serialises that dict through a generated protobuf
   module (utils/proto/fiksProto_pb2), which is not part of this build: records are written as JSON.
+  `only_deltas` writes the differences between consecutive episodes (DeepDiff when importable, else a
+  built-in structural diff with DeepDiff's report keys); `save_occupation_map` writes the agents' cell-visit
+  counts over the level (.npy, plus a .png heatmap when matplotlib is importable; the reference sums into a
+  fixed 15x15 array from a key its summary does not have, recorder.py:171-187); `save_trajectory_map` raises
+  NotImplementedError like the reference (recorder.py:189-190).
 * `BatchedEpisodeLog` -- the batched counterpart: per-episode returns/lengths of a `VectorFactory`,
   collected from its step infos without per-step host copies of the whole batch.
 """
@@ -72,7 +78,8 @@ class EnvMonitor(_Wrapper):
         with filepath.open('wb') as f:
             pickle.dump(self._monitor_df.reset_index(), f, protocol=pickle.HIGHEST_PROTOCOL)
         if auto_plotting_keys:
-            raise NotImplementedError('plotting (utils/plotting) is not part of this build')
+            from .plotting import plot_single_run
+            plot_single_run(filepath, column_keys=auto_plotting_keys)
 
     def report_possible_colum_keys(self):
         print(self._monitor_df.columns)
@@ -117,14 +124,89 @@ class EnvRecorder(_Wrapper):
                 'header': self.env.summarize_header()}
 
     def save_records(self, filepath=None, only_deltas=False, save_occupation_map=False, save_trajectory_map=False):
-        if only_deltas or save_occupation_map or save_trajectory_map:
-            raise NotImplementedError('deltas (deepdiff) and occupation/trajectory plots are not part of this build')
         self._finalize()
         filepath = Path(filepath or self.filepath)
         filepath.parent.mkdir(exist_ok=True, parents=True)
+        rec = self.records()
+        if only_deltas:
+            eps = rec['episodes']
+            rec['episodes'] = [_deltas(a, b) for a, b in zip(eps, eps[1:])]
         with filepath.open('w') as f:
-            json.dump(self.records(), f)
+            json.dump(rec, f, default=str)
+        if save_occupation_map:
+            self.occupation_map(filepath.with_name(filepath.stem + '_occupation'))
+        if save_trajectory_map:
+            raise NotImplementedError('This has not yet been implemented.')  # as the reference (recorder.py:189-190)
         return filepath
+
+    def occupation_map(self, out_stem=None):
+        """[H, W] counts of agent positions over every recorded step (recorder.py:171-180, over the level's
+        shape); with out_stem, written to <out_stem>.npy and, if matplotlib is importable, <out_stem>.png."""
+        import numpy as np
+        H, W = self.env.spec.H, self.env.spec.W
+        occ = np.zeros((H, W), np.int64)
+        for ep in self._recorder_out_list:
+            for st in ep['steps']:
+                for a in st.get('agents', []):
+                    if 0 <= a['x'] < H and 0 <= a['y'] < W:
+                        occ[a['x'], a['y']] += 1
+        if out_stem is not None:
+            out_stem = Path(out_stem)
+            np.save(out_stem.with_suffix('.npy'), occ)
+            try:
+                import matplotlib
+                matplotlib.use('Agg')
+                import matplotlib.pyplot as plt
+            except Exception:
+                return occ
+            fig, ax = plt.subplots(figsize=(6, 6 * H / max(W, 1) + 0.5))
+            im = ax.imshow(occ, cmap='viridis')
+            fig.colorbar(im, ax=ax)
+            ax.set_title('agent occupation')
+            fig.savefig(out_stem.with_suffix('.png'))
+            plt.close(fig)
+        return occ
+
+
+def _deltas(t1, t2):
+    """Differences between two episode records: DeepDiff(t1, t2, ignore_order=True) (recorder.py:91-95) when
+    deepdiff is importable, else a structural diff reporting DeepDiff's keys for ordered data
+    (values_changed, type_changes, dictionary_item_added/removed, iterable_item_added/removed)."""
+    try:
+        from deepdiff import DeepDiff
+        return json.loads(DeepDiff(t1, t2, ignore_order=True).to_json())
+    except ImportError:
+        pass
+    out = {}
+
+    def put(kind, path, val):
+        out.setdefault(kind, {})[path] = val
+
+    def walk(a, b, path):
+        if isinstance(a, dict) and isinstance(b, dict):
+            for k in a:
+                if k not in b:
+                    put('dictionary_item_removed', f"{path}['{k}']", a[k])
+                else:
+                    walk(a[k], b[k], f"{path}['{k}']")
+            for k in b:
+                if k not in a:
+                    put('dictionary_item_added', f"{path}['{k}']", b[k])
+        elif isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)):
+            for i in range(min(len(a), len(b))):
+                walk(a[i], b[i], f'{path}[{i}]')
+            for i in range(len(b), len(a)):
+                put('iterable_item_removed', f'{path}[{i}]', a[i])
+            for i in range(len(a), len(b)):
+                put('iterable_item_added', f'{path}[{i}]', b[i])
+        elif type(a) is not type(b):
+            put('type_changes', path, {'old_type': type(a).__name__, 'new_type': type(b).__name__,
+                                       'old_value': a, 'new_value': b})
+        elif a != b:
+            put('values_changed', path, {'old_value': a, 'new_value': b})
+
+    walk(t1, t2, 'root')
+    return out
 
 
 class BatchedEpisodeLog:

@@ -259,6 +259,11 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None, custom_mo
     with open(config_path) as f:
         cfg = yaml.safe_load(f)
     gen = cfg['General']
+    if not gen.get('individual_rewards', True):
+        # Q26: with individual_rewards false the reference's Factory.step always raises (factory.py:217 sums the
+        # float that summarize_step_results returns, :256-259), so that mode has no behaviour to reproduce
+        raise UnsupportedSpec('individual_rewards: false crashes Factory.step in the reference (Q26, '
+                              'environment/factory.py:217); only individual rewards are supported')
     level_name = gen['level_name']
     lvl = Path(custom_level_path) if custom_level_path else LEVELS_DIR / f'{level_name}.txt'
     H, W, level, floor, walls, doors = _parse_level(lvl)

@@ -209,3 +209,34 @@ def test_monitor_and_recorder_on_engine(tmp_path):
     assert len(env.env.monitor_df) >= 1
     out = json.loads(env.save_records().read_text())
     assert out['episodes'][0]['steps'][0]['step'] == 1
+
+
+def test_env_recorder_deltas_and_occupation(tmp_path):
+    import numpy as np
+    from mfg_amd.monitor import EnvRecorder, _deltas
+    f = _ScriptedFactory()
+    f.spec = type('S', (), {'H': 12, 'W': 3})()
+    r = EnvRecorder(f, tmp_path / 'rec.json')
+    r.reset()
+    for _ in range(8):
+        r.step([0])
+    out = json.loads(r.save_records(only_deltas=True, save_occupation_map=True).read_text())
+    assert len(out['episodes']) == 1  # one delta between the two recorded episodes
+    d = out['episodes'][0]
+    assert d['values_changed']["root['steps'][0]['step']"] == {'old_value': 1, 'new_value': 5}
+    occ = np.load(tmp_path / 'rec_occupation.npy')
+    assert occ.shape == (12, 3) and occ.sum() == 8 and occ[1:9, 0].tolist() == [1] * 8
+    assert _deltas({'a': [1, 2]}, {'a': [1], 'b': 0}) == {'iterable_item_removed': {"root['a'][1]": 2},
+                                                        'dictionary_item_added': {"root['b']": 0}}
+    with pytest.raises(NotImplementedError):
+        r.save_records(save_trajectory_map=True)
+
+
+def test_env_monitor_auto_plot(tmp_path):
+    from mfg_amd.monitor import EnvMonitor
+    m = EnvMonitor(_ScriptedFactory(), tmp_path / 'mon.pick')
+    m.reset()
+    for _ in range(8):
+        m.step([0])
+    m.save_monitor(auto_plotting_keys=['Agent[a]_North'])
+    assert (tmp_path / 'mon.png').exists() or (tmp_path / 'mon.csv').exists()

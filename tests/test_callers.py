@@ -48,6 +48,19 @@ def test_config_explainer_lists_what_compiles(tmp_path, compat_path):
     assert set(ce.get_actions()) == set(S._ACTIONS) | set(S._MOVE_GROUPS)
 
 
+def test_config_explainer_lists_custom_rules(compat_path):
+    """utils/tools.py:24-39: a custom path adds its Rule classes (explained by their __init__ defaults); they
+    run on the host beside the engine (custom_modules_path)."""
+    from pathlib import Path
+    from marl_factory_grid.utils.tools import ConfigExplainer
+    from mfg_amd import spec as S
+    rules = ConfigExplainer(Path(__file__).parent / 'custom_rules').get_rules()
+    assert rules['DoneWhenCrowded'] == {'k': 3, 'reward': -1.0}
+    assert rules['DoorProximityBonus'] == {'bonus': 0.05}
+    assert set(rules) == set(S._RULES) | set(S._DEST_SPAWNRULES) | {
+        'DoorProximityBonus', 'CountFailedActions', 'PenaltyBeforeActions', 'DoneWhenCrowded'}
+
+
 def test_plot_single_run_from_monitor_file(tmp_path):
     import pandas as pd
     import pickle

@@ -186,3 +186,47 @@ def test_two_shards_equal_one_engine(cfg, B, steps):
     assert torch.equal(torch.cat([shards[0].export_state(), shards[1].export_state()]), st)
     for e in [full] + shards:
         e.close()
+
+
+@pytest.mark.parametrize('auto_reset', [False, True])
+def test_out_of_range_action_crashes_only_that_env(auto_reset):
+    """An action index outside [0, n_actions[a]) is the reference's IndexError (factory.py:201-206): that env
+    reports MFG_CRASH_ACTION + done and takes no step; every other env steps exactly like the oracle. With
+    auto-reset the crashed env is reset and steps normally afterwards."""
+    import oracle as O
+    from mfg_amd import abi
+    B = 8  # noqa: N806
+    torch, spec, eng = _engine('large8.yaml', B)
+    A = spec.n_agents
+    buf = _buffers(torch, eng, 1, torch.float64)
+    eng.reset(obs=buf['obs'][0], init=True, seed_base=0)
+    envs = [O.OracleEnv(spec, i) for i in range(B)]
+    for e in envs:
+        e.reset()
+    rng = np.random.default_rng(5)
+    # agent 0: nothing acts before the IndexError, so a reset env matches a fresh oracle reset (agents ahead of a
+    # bad index do act first, as in the reference's ordered loop, which the oracle does not model)
+    bad = {3: (0, spec.n_actions[0]), 5: (0, -1)}
+    for t in range(3):
+        acts = np.stack([rng.integers(0, spec.n_actions[a], size=B) for a in range(A)], 1).astype(np.int32)
+        if t == 0:
+            for env, (a, v) in bad.items():
+                acts[env, a] = v
+        eng.step(1, actions=torch.as_tensor(acts, device=eng.device), reward=buf['reward'], done=buf['done'],
+                 obs=buf['obs'], ev_act=buf['ev_act'], ev_watch=buf['ev_watch'], ev_misc=buf['ev_misc'],
+                 auto_reset=auto_reset)
+        rew, done = buf['reward'][0].cpu().numpy(), buf['done'][0].cpu().numpy()
+        flags = buf['ev_misc'][0, :, abi.EVM_FLAGS].cpu().numpy()
+        for i in range(B):
+            crashed_now = t == 0 and i in bad
+            if crashed_now or (t > 0 and i in bad and not auto_reset):
+                assert done[i] == 1 and (flags[i] >> 1) & 1, (t, i)
+                assert (flags[i] >> 8) & 0xFF == 8  # MFG_CRASH_ACTION (include/mfg.h)
+                continue
+            r, d, _ = envs[i].step(acts[i])
+            assert list(rew[i]) == list(r) and bool(done[i]) == bool(d), (t, i)
+            assert not (flags[i] >> 1) & 1, (t, i)
+        if t == 0 and auto_reset:
+            for i in bad:  # the engine reset them after the crash: the oracle does the same
+                envs[i].reset()
+    eng.close()

@@ -109,3 +109,21 @@ def test_factory_with_custom_rules_matches_reference(seed, compat_path):
         if done:
             env.reset()
     env.close() if hasattr(env, 'close') else None
+
+
+def test_builtin_name_wins_over_a_custom_class(tmp_path, compat_path):
+    """The reference searches its built-in folders before custom_modules_path (config_parser.py:213-233), so a
+    custom class named like a built-in rule is never used; compile_spec keeps the built-in on the device."""
+    import shutil
+    from mfg_amd.spec import compile_spec
+    custom = tmp_path / 'custom'
+    shutil.copytree(CUSTOM, custom)
+    (custom / 'shadow.py').write_text(
+        "from marl_factory_grid.environment.rules import Rule\n\n\n"
+        "class WatchCollisions(Rule):\n"
+        "    def tick_post_step(self, state):\n"
+        "        raise AssertionError('the shadowing custom class must not be used')\n")
+    spec = compile_spec(CFG, custom_modules_path=str(custom))
+    names = [n for _, n, _, _ in spec.host_rules]
+    assert 'WatchCollisions' not in names
+    assert names == ['PenaltyBeforeActions', 'CountFailedActions', 'DoorProximityBonus', 'DoneWhenCrowded']

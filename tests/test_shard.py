@@ -86,3 +86,40 @@ def test_gloo_world2_matches_single_process():
     for _, _, metrics in got:
         assert metrics[1] == world * PER_RANK * STEPS
         assert abs(metrics[0] - total) < 1e-9
+
+
+ROOT = __import__('pathlib').Path(__file__).resolve().parent.parent
+
+
+def _bench(*args, timeout=240):
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    env.pop('WORLD_SIZE', None)
+    return subprocess.run([sys.executable, str(ROOT / 'bench.py'), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=str(ROOT))
+
+
+def test_bench_spawns_ranks_and_collects_rank0_line():
+    """`bench.py --gpus 2` (the driver's SCALE command form) starts 2 rank processes itself, joins them in one
+    process group (gloo rehearsal: --dry-run), takes the MAX over ranks and prints exactly one JSON line."""
+    import json
+    p = _bench('--gpus', '2', '--dry-run', '--steps', '5', '--batch', '8')
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['n_ranks_rccl'] == 2 and d['dry_run']
+    assert d['env_ranges'] == [[0, 8], [8, 8]]
+    assert d['metrics_allreduce'] == 2 * 8 * 5
+    assert 'launcher' in d
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    import torch
+    visible = torch.cuda.device_count()
+    n = max(2, visible + 1)
+    p = _bench('--gpus', str(n), '--steps', '2', '--warmup', '0', '--no-cpu-baseline')
+    assert p.returncode == 2
+    assert f'{n} GPUs requested, {visible} visible' in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith('{')]

@@ -48,6 +48,12 @@ def test_unsupported_classes_are_rejected(tmp_path):
                    "Entities: {}\nRules: {Defaults: {}}\n")
     with pytest.raises(UnsupportedSpec):
         compile_spec(bad)
+    # Q26: global (non-individual) rewards crash the reference's step; rejected, not silently mis-summed
+    bad.write_text("General: {env_seed: 69, individual_rewards: false, level_name: large, pomdp_r: 3}\n"
+                   "Agents: {W: {Actions: [Noop], Observations: [Walls]}}\n"
+                   "Entities: {}\nRules: {}\n")
+    with pytest.raises(UnsupportedSpec, match='individual_rewards'):
+        compile_spec(bad)
 
 
 def _header_functions():

@@ -25,7 +25,7 @@ def main():
     from mfg_amd.factory import BatchedFactory
     from mfg_amd.marl import BatchedA2C
     f = BatchedFactory(args.config, args.batch, seed_base=0)
-    tr = BatchedA2C(f, n_steps=args.n_steps, check_cap=False)
+    tr = BatchedA2C(f, n_steps=args.n_steps, check_cap=True)
     tr.train(2)  # warm-up (allocations, kernels)
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -32,16 +32,21 @@ CUSTOM = REPO / 'tests' / 'custom_rules'
 
 # The reference's own loader cannot load a custom rule: _load_smth exits when BOTH built-in folders miss
 # (`if (e1 and e2) or e3`, config_parser.py:238), even after the custom path found the class. The fixture
-# records what the reference does once that lookup succeeds: names defined in the custom module resolve there
-# first; everything else goes through the unchanged reference lookup.
+# records what the reference does once that lookup succeeds, in the reference's own search order: the
+# built-in folders first (environment/, then modules/), the custom path last. A custom class that shadows a
+# built-in name therefore resolves to the built-in, exactly as compile_spec / locate_custom_class do.
 _orig_locate = _cp.locate_and_import_class
 
 
 def _locate(name, folder=''):
     try:
-        return _orig_locate(name, CUSTOM)
-    except AttributeError:
         return _orig_locate(name, folder)
+    except AttributeError:
+        if Path(str(folder)).name != 'modules' or Path(str(folder)) == CUSTOM:
+            raise
+        # both built-in folders missed: answer with the custom path's class from the second built-in lookup,
+        # so _load_smth sees e2 = None and keeps it instead of exiting
+        return _orig_locate(name, CUSTOM)
 
 
 _cp.locate_and_import_class = _locate

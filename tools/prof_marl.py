@@ -14,7 +14,7 @@ def main():
     from mfg_amd.marl import BatchedA2C
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
     f = BatchedFactory('large8.yaml', B, seed_base=0)
-    tr = BatchedA2C(f, n_steps=5, check_cap=False)
+    tr = BatchedA2C(f, n_steps=5, check_cap=True)
     tr.train(2)
     torch.cuda.synchronize()
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
