@@ -4,10 +4,7 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/ablate
-VARS=${*:-NOSWAP NODEBT NOOBS}
-for v in $VARS; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -shared -fPIC -DMFG_ABLATE_$v \
-    -o build/ablate/libmfg_hip_$v.so marl-factory-grid_amd/csrc/mfg_engine.hip &
+for v in ${*:-NOSWAP NODEBT NOOBS}; do
+  ./tools/build_lib.sh build/ablate/libmfg_hip_$v.so -DMFG_ABLATE_$v
 done
-wait
 ls build/ablate

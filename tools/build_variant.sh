@@ -1,10 +1,11 @@
 #!/bin/bash
-# Exact engine variants for A/B timing (tools/ab_run.sh): build/ablate/libmfg_hip_VARIANT.so with -DMFG_VARIANT.
+# Engine variants for A/B timing (tools/ab_run.sh): build/ablate/libmfg_hip_NAME.so from "NAME=FLAGS" arguments,
+# e.g. tools/build_variant.sh RPV7=-DMFG_RPV=7 OVL0=-DMFG_RESET_OVERLAP=0 (one variant at a time: each build is
+# already 5 parallel compiles).
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/ablate
-for v in "$@"; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -shared -fPIC -DMFG_$v \
-    -o build/ablate/libmfg_hip_$v.so marl-factory-grid_amd/csrc/mfg_engine.hip &
+for arg in "$@"; do
+  name=${arg%%=*}; flags=${arg#*=}
+  ./tools/build_lib.sh build/ablate/libmfg_hip_$name.so $flags
 done
-wait
