@@ -353,9 +353,10 @@ def main():
     step_no = 0
     episodes = torch.zeros((), dtype=torch.float64, device=dev)
 
-    def run(n, events=None, profile=False, obs_buf=None):
+    def run(n, events=None, profile=False, obs_buf=None, after=None):
         """n steps in calls of F (the last call may be shorter). Per-kernel HIP events are recorded only
-        around full-K calls, so the per-launch roofline figures are always those of K=F launches."""
+        around full-K calls, so the per-launch roofline figures are always those of K=F launches.
+        after(k): work run on the stream after each call (the dense obs consumer of the packed comparison)."""
         nonlocal step_no
         done_steps = 0
         while done_steps < n:
@@ -368,6 +369,8 @@ def main():
             eng.step(k, actions=None, philox_seed=12345, env_base=env_base, step_base=step_no, reward=rew, done=done,
                      obs=obs if obs_buf is None else obs_buf, ev_act=ev_a, ev_watch=ev_w, ev_misc=ev_m,
                      auto_reset=True)
+            if after is not None:
+                after(k)
             if events is not None:
                 e.record(stream)
                 events.append((s, e, k))
@@ -398,15 +401,15 @@ def main():
         dist.all_reduce(episodes)  # optional metrics all-reduce (tiny, latency-bound)
     total = B * world * args.steps
     value = total / elapsed
-    def timed(n, obs_buf):
+    def timed(n, obs_buf, after=None):
         """n more steps into obs_buf, timed like the headline (barrier + synchronize brackets, max over ranks)."""
-        run(F, obs_buf=obs_buf)
+        run(F, obs_buf=obs_buf, after=after)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
-        run(n, obs_buf=obs_buf)
+        run(n, obs_buf=obs_buf, after=after)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -446,7 +449,19 @@ def main():
         el3 = timed(packed_steps, po)
         pk_bytes = core_bytes(spec) + A * (4 + 6 * args.cap + 4 * args.emb)
         pv = B * world * packed_steps / el3
+        # what packed replaces: dense f32 obs + the policy's obs_proj over them (one GEMM per call on the same
+        # stream, hipBLASLt), i.e. the policy input from materialised obs
+        emb_d = torch.empty((F * B * A, args.emb), device=dev)
+        wt = w.t().contiguous()
+
+        def proj(k):
+            torch.matmul(obs[:k].reshape(k * B * A, -1), wt, out=emb_d[:k * B * A])
+        el4 = timed(packed_steps, None, after=proj)
+        dv = B * world * packed_steps / el4
+        del emb_d
         packed = {"obs": f"packed (cap {args.cap}) + fused obs_proj (E {args.emb}, f32)", "value": round(pv, 1),
+                  "dense_f32_plus_proj": {"value": round(dv, 1), "ms_per_step": round(el4 / packed_steps * 1e3, 4),
+                                          "what": "dense f32 obs, then obs_proj as one f32 GEMM per call"},
                   "unit": "env-steps/s", "steps": packed_steps, "ms_per_step": round(el3 / packed_steps * 1e3, 4),
                   "algo_bytes_per_env_step": pk_bytes,
                   "pipeline_GBs": round(pv / world * pk_bytes / 1e9, 2),

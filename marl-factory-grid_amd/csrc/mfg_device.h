@@ -71,6 +71,7 @@ struct MfgLayout {
   int32_t o_battery, o_frozen_bat, o_dirt_amt, o_pcg, o_mt, o_perm;
   int32_t o_machines, o_maints;       // lean part: group tables (pos | flags words)
   int32_t o_mstate, o_mpath, o_grank; // after perm: maintainer state, paths (u16 cells), graph ranks (u16)
+  int32_t o_logic;                    // end of the step prefix (k_logic stages [0, o_logic); 16-B aligned)
 };
 // per-maintainer state ints: [path_n, path_head, next_n, last_serviced, next[mmax + 1]]
 enum { MS_PATH_N = 0, MS_PATH_HEAD, MS_NEXT_N, MS_LAST_SERVICED, MS_NEXT };

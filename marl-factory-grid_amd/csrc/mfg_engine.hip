@@ -32,6 +32,7 @@ struct mfg_engine {
   bool overlap = false;     // resets beside the render (MFG_RESET_OVERLAP)
   bool replay_each = false; // pay the shuffle debt after every step, not once per call (long resets + in-step RNG)
   int obs_nwv = 1;          // waves per env of the render (> 1: multi-wave render, k_obs_mw)
+  bool replay2 = false;     // two-wave replay (k_replay2) for floor lists whose 1-wave slice fills a SIMD
   hipStream_t ov_stream = nullptr;  // MFG_ABLATE_OVERLAP measurement only (timing of a replay overlapped with the next call)
   hipEvent_t ov_ev = nullptr;
   struct Mark { int k; hipEvent_t a, b; };
@@ -158,16 +159,17 @@ static int align_up(int x, int a) { return (x + a - 1) / a * a; }
 
 static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int dropmax, int destmax, int mmax,
                         int kmax, int mstate_ints, int path_cap, int graph, int dirt_cap) {
+  // [0, o_logic): what a step reads and writes (k_logic stages only this prefix); [o_logic, o_mt): the
+  // per-episode values only the render reads (frozen ray origins, positions, batteries, Q11/Q12); then the RNG
+  // streams and the maintainer tail. Rule counters: one per rule of the spec.
   int o = 0;
   const int A = s->n_agents, nd = s->n_doors;
   const int dm = dirt_cap;
   L->o_hdr = o; o += 4 * MFG_HDR_N;
-  L->o_rule_ctr = o; o += 4 * MFG_MAX_RULES;
+  L->o_rule_ctr = o; o += 4 * std::max(1, s->n_rules);
   L->o_agent_pos = o; o += 4 * A;
   L->o_agent_arr = o; o += 4 * A;
   L->o_agent_par = o; o += 4 * A;
-  L->o_frozen_org = o; o += 4 * A;
-  L->o_frozen_gp = o; o += 4 * A;
   L->o_door = o; o += 4 * nd;
   L->o_items = o; o += 4 * imax;
   L->o_pods = o; o += 4 * pmax;
@@ -179,9 +181,14 @@ static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int
   L->o_dirt_id = o; o += 4 * dm;
   o = align_up(o, 8);
   L->o_battery = o; o += 8 * A;
-  L->o_frozen_bat = o; o += 8 * A;
   L->o_dirt_amt = o; o += 8 * dm;
   L->o_pcg = o; o += 8 * 4;
+  o = align_up(o, 16);
+  L->o_logic = o;
+  L->o_frozen_org = o; o += 4 * A;
+  L->o_frozen_gp = o; o += 4 * A;
+  o = align_up(o, 8);
+  L->o_frozen_bat = o; o += 8 * A;
   o = align_up(o, 16);
   L->o_mt = o; o += 4 * 624;
   L->o_perm = o; o += 2 * s->n_floor;
@@ -263,9 +270,12 @@ static int validate_spec(const mfg_spec* s) {
   if (s->n_doors < 0 || s->n_doors > MFG_MAX_DOORS) return fail("too many doors");
   if (s->n_floor < 1 || s->n_floor > s->H * s->W || !s->floor_cells) return fail("n_floor out of range");
   if (s->n_walls < 0 || s->n_walls > s->H * s->W) return fail("n_walls out of range");
-  if (s->pomdp_r < 0 || s->pomdp_r > 8) return fail("engine supports pomdp_r in [0,8]");
-  if (s->pomdp_r == 0 && (std::min(s->H, s->W) > 30 || s->H * s->W > 4095))
-    return fail("full observability (pomdp_r 0) needs min(H, W) <= 30 and H*W < 4096");
+  // the ray radius is the window diameter (Q13): 2 r + 1, or min(H, W) with full observability; a ray holds
+  // radius + 1 points and the walk keeps them in 32-bit masks (the per-agent tables must also fit the LDS,
+  // checked below)
+  if (s->pomdp_r < 0 || s->pomdp_r > 15) return fail("engine supports pomdp_r in [0, 15] (rays of <= 32 points)");
+  if (s->pomdp_r == 0 && std::min(s->H, s->W) > 31)
+    return fail("full observability (pomdp_r 0) needs min(H, W) <= 31 (rays of <= 32 points)");
   for (int a = 0; a < s->n_agents; a++) {
     if (s->n_positions[a] < 0 || s->n_positions[a] > MFG_MAX_POSITIONS) return fail("n_positions out of range");
     for (int k = 0; k < s->n_positions[a]; k++)
@@ -453,7 +463,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     h.max_pairs = std::max(16, 2 * tot_cap + 3 * tot_cap);
   }
   h.pair_pool = nullptr;
-  h.lds_logic = h.step_rng ? h.lds_full : align_up(h.L.o_mt, 16) + 4 * MFG_WAVE;  // + per-door count scratch
+  h.lds_logic = h.step_rng ? h.lds_full : h.L.o_logic + 4 * MFG_WAVE;  // step prefix + per-door count scratch
   h.fv_words = align_up((2 * h.fr + 1) * (2 * h.fr + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
@@ -671,6 +681,11 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     }
     e->rpd_blocks = std::max(1, per_cu) * std::max(1, n_cu);
     e->n_cu = std::max(1, n_cu);
+#ifndef MFG_REPLAY2
+#define MFG_REPLAY2 1  // 0: never, 1: when the 1-wave replay slice leaves <= 2 waves per SIMD, 2: always
+#endif
+    e->replay2 = h.xchg_ordered && (size_t)h.lds_replay_per_wave + RP2_RING <= MFG_LDS_MAX &&
+                 (MFG_REPLAY2 == 2 || (MFG_REPLAY2 == 1 && MFG_LDS_MAX / (size_t)h.lds_replay_per_wave <= 8));
     e->overlap = MFG_RESET_OVERLAP == 2 || (MFG_RESET_OVERLAP == 1 && (long long)h.A * h.nf >= 16384);
     // with long resets (overlap) and a rule that consumes the floor order inside a step, the envs that finish
     // or respawn dirt would otherwise pay up to K steps of debt on the critical path (C4: 6.7 -> 7.4M env-steps/s)
@@ -728,7 +743,8 @@ extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
                        L.o_dirt_id, L.o_battery, L.o_frozen_bat, L.o_dirt_amt, L.o_pcg, L.o_mt, L.o_perm,
                        e->h.lmax, e->h.obs_agent_stride, e->h.lds_full, e->h.xchg_ordered, L.o_machines,
                        L.o_maints, L.o_mstate, L.o_mpath, L.o_grank, e->h.dirt_cap, e->h.lds_logic, e->h.lds_obs,
-                       e->h.lds_replay_per_wave, e->h.bfs_off, e->h.bfs_bytes, e->h.max_pairs, e->h.scratch_bytes};
+                       e->h.lds_replay_per_wave, e->h.bfs_off, e->h.bfs_bytes, e->h.max_pairs, e->h.scratch_bytes,
+                       L.o_logic};
   const int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
@@ -877,9 +893,14 @@ static int replay_impl(mfg_engine* e, void* stream) {
     hipLaunchKernelGGL(k_rp_place, dim3(g256), dim3(256), 0, st, (long long)e->B, e->rp_hist, e->rp_key,
                        e->rp_order);
   }
-  hipLaunchKernelGGL(k_replay, dim3((unsigned)((e->B + wpb - 1) / wpb)), dim3(wpb * 64),
-                     (size_t)e->h.lds_replay_per_wave * wpb, st, e->d_spec, e->d_state,
-                     (long long)e->B, lpt ? (const int*)e->rp_order : nullptr);
+  if (e->replay2)  // large floor lists: a producer and a consumer wave per env (replay_env2)
+    hipLaunchKernelGGL(k_replay2, dim3((unsigned)e->B), dim3(2 * MFG_WAVE),
+                       (size_t)e->h.lds_replay_per_wave + RP2_RING, st, e->d_spec, e->d_state, (long long)e->B,
+                       lpt ? (const int*)e->rp_order : nullptr);
+  else
+    hipLaunchKernelGGL(k_replay, dim3((unsigned)((e->B + wpb - 1) / wpb)), dim3(wpb * 64),
+                       (size_t)e->h.lds_replay_per_wave * wpb, st, e->d_spec, e->d_state,
+                       (long long)e->B, lpt ? (const int*)e->rp_order : nullptr);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
   PROF_END(e, st, MFG_K_REPLAY);

@@ -31,6 +31,15 @@
 // SpawnAgents, C4/C5), 2 always
 #define MFG_RESET_OVERLAP 1
 #endif
+#ifndef MFG_RESET_DRAWS
+#define MFG_RESET_DRAWS 1  // SpawnAgents' shuffle(empty_positions) draws on replay_shuffle_t (0: mt_randbelow_seq)
+#endif
+#ifndef MFG_PK_WPE
+#define MFG_PK_WPE 7  // waves per SIMD asked of the short-ray packed render (1: no request)
+#endif
+#ifndef MFG_OBS_CLAMP
+#define MFG_OBS_CLAMP 1  // k_obs dense placement: lanes past the window duplicate the last cell (no store masks)
+#endif
 #ifndef MFG_RPV
 #define MFG_RPV 3  // k_replay swap-block variant bits (exact; see replay_shuffle_t)
 #endif
@@ -413,10 +422,12 @@ static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice")
 // 18..31 of the tempered word, which the last tempering step (y ^= y >> 18) leaves unchanged.
 // SWAP = false: the draws of a shuffle of hi + 1 elements only (randbelow(i + 1) for i = hi .. 1, no
 // permutation), e.g. shuffle(empty_positions) in the reset, on the same chunked path.
+// Returns j of the first accepted draw (i == hi) when SWAP is false (random.shuffle(list); list.pop() takes it).
 template <bool TOP14, bool SWAP = true>
-__device__ void replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
+__device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
+  int first_j = -1;
   uint16_t* sink = (uint16_t*)e.scratch + lane;  // 128 B: one u16 per lane
   uint32_t* ptab = e.stab;
   const int lo = 1;
@@ -476,6 +487,7 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     const int inext = icur - nacc, idxn = idx + consumed;
 #ifndef MFG_ABLATE_NOSWAP
     if constexpr (!SWAP) {
+      if (first_j < 0 && m) first_j = rl((int)r, ffs64(m));
       if (idxn <= 560) yw = mt[idxn + lane];
     } else {
     // (a chunk with no accepted draw runs the block on the sinks: rare, and one branch less per chunk)
@@ -573,10 +585,130 @@ __device__ void replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   if (SWAP && lane == 0) e.stab[RP_CTR] = ctr;
   e.setH(H_MT_IDX, idx);
   wave_sync();
+  return first_j;
 }
 __device__ __forceinline__ void replay_shuffle(const Env& e, uint16_t* perm) {
   if (e.S->replay_top14) replay_shuffle_t<true>(e, perm, e.S->nf - 1);
   else replay_shuffle_t<false>(e, perm, e.S->nf - 1);
+}
+
+// ---- two-wave replay (large floor lists: the 1-wave replay slice leaves <= 2 waves per SIMD) ----------------
+// The draws of a shuffle (MT words, tempering, acceptance) never read the permutation, so one wave (the
+// producer) runs them ahead for all of an env's debt while a second wave (the consumer) applies the swap blocks:
+// per chunk the producer writes (icur, nacc) and the accepted draws' j in rank order to a ring in LDS; the two
+// waves meet at one workgroup barrier per RP2_R chunks (double-buffered ring). Exactly the single-wave
+// replay's arithmetic: the producer is replay_shuffle_t's draw half, the consumer its swap half with lane = rank.
+#define RP2_R 16                       // chunks per ring half
+#define RP2_REC (4 + 2 * MFG_WAVE)     // bytes per chunk record: icur | nacc << 16, then j[64] (u16)
+#define RP2_RING (2 * RP2_R * RP2_REC + 16)  // both halves + [0] per-half chunk count x 2, [2] done phase
+struct Rp2Prod {  // producer state carried across ring phases
+  int s, icur, idx;
+  uint32_t yw;
+};
+template <bool TOP14>
+__device__ void rp2_produce(const Env& e, uint8_t* half, int* cnt, Rp2Prod& st, int d, int hi) {
+  uint32_t* mt = e.mt();
+  const int lane = e.lane, lo = 1;
+  int n = 0;
+  while (n < RP2_R && st.s < d) {
+    if (st.idx > 560) {
+      if (st.idx >= 624) {
+        mt_twist(e);
+        st.idx -= 624;
+      }
+      const int jw = st.idx + lane;
+      if (st.idx <= 560) {
+        st.yw = mt[jw];
+      } else {
+        const int jn = jw >= 624 ? jw - 624 : 0;
+        const uint32_t nw = mt_mix(mt[jn], mt[jn + 1], mt[jn + 397]);
+        st.yw = jw < 624 ? mt[jw < 624 ? jw : 0] : nw;
+      }
+    }
+    const int icur = st.icur;
+    const uint32_t y = TOP14 ? mt_temper3(st.yw) : mt_temper(st.yw);
+    const int sh = __clz(icur + 1);
+    const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);
+    const uint32_t r = y >> sh;
+    const int c = min(icur - (int)r, span);
+    u64 m = ballot(c >= lane);
+    int A;
+    for (;;) {
+      A = mbcnt(m);
+      const u64 m2 = ballot(A <= c);
+      if (m2 == m) break;
+      m = m2;
+    }
+    const int consumed = popc(ballot(A <= span));
+    const int nacc = popc(m);
+    uint8_t* rec = half + n * RP2_REC;
+    if (lanes(m)) ((uint16_t*)(rec + 4))[A] = (uint16_t)r;
+    if (lane == 0) *(int*)rec = icur | (nacc << 16);
+    const int idxn = st.idx + consumed;
+    if (idxn <= 560) st.yw = mt[idxn + lane];
+    st.idx = idxn;
+    st.icur = icur - nacc;
+    n++;
+    if (st.icur < lo) {  // this shuffle is done: the next one starts at the top
+      st.s++;
+      st.icur = hi;
+    }
+  }
+  if (lane == 0) *cnt = n;
+}
+__device__ void rp2_consume(const Env& e, const uint8_t* half, int n, uint32_t& ctr) {
+  uint16_t* perm = e.perm();
+  const int lane = e.lane;
+  uint16_t* sink = (uint16_t*)e.scratch + lane;
+  uint32_t* ptab = e.stab;
+  // the half's chunk headers, lane q = chunk q (read per chunk with v_readlane, off the LDS chain)
+  const int hds = lane < n ? *(const int*)(half + lane * RP2_REC) : 0;
+  for (int q = 0; q < n; q++) {
+    const uint8_t* rec = half + q * RP2_REC;
+    const int hd = rl(hds, q);
+    const int icur = hd & 0xFFFF, nacc = hd >> 16;
+    if (!nacc) continue;
+    const bool acc = lane < nacc;
+    const int A = lane;
+    // j and the value leaving i are read together (one LDS round trip)
+    const int jraw = (int)((const uint16_t*)(rec + 4))[lane];
+    uint16_t* const ptop = perm + icur;
+    uint16_t* pi = ptop - min(A, nacc);  // lanes past the block read the next block's top (a broadcast)
+    int v = (int)*pi;
+    const int j = acc ? jraw : icur;
+    const int i = icur - A, inext = icur - nacc;
+    const u64 m = ballot(acc);
+    u64 cm = ballot(j > inext) & ballot(j < i) & m;
+    if (cm) {
+      if (popc(cm) <= RP_SERIAL_FWD) {
+        const int keyv = icur - j;
+        do {
+          const int s2 = ffs64(cm);
+          asm volatile("s_bitset0_b64 %0, %1" : "+s"(cm) : "s"(s2));
+          const int key = rl(keyv, s2);
+          const int vs = rl(v, s2);
+          v = A == key ? vs : v;
+        } while (cm);
+      } else {
+        const bool fwd = lanes(cm);
+        ctr++;
+        const uint32_t tag = ctr << 6;
+        atomicMax(&ptab[fwd ? icur - j : lane], fwd ? tag | (uint32_t)lane : 0u);
+        wave_sync();
+        const uint32_t tp = ptab[A & 63];
+        int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
+        while (ballot(ptr >= 0)) {
+          const int src = ptr >= 0 ? ptr : lane;
+          const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
+          if (ptr >= 0) { v = v2; ptr = p2; }
+        }
+      }
+    }
+    uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
+    F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
+    if (acc) *pi = (uint16_t)F;
+    wave_sync();
+  }
 }
 
 // random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
@@ -1920,10 +2052,16 @@ __device__ void env_reset(const Env& e, int* scratch) {
       for (int b = 0; b < a; b++) occ |= rl(my_cell, b) == cell;
       return !occ;
     };
+#if MFG_RESET_DRAWS
+    // the draws of shuffle(empty_positions) on the replay's branch-free chunked path; the first accepted draw
+    // (i = m - 1) picks the slot pop() takes
+    const int j = m < 2 ? (m == 1 ? 0 : -1)
+                        : (S->replay_top14 ? replay_shuffle_t<true, false>(e, nullptr, m - 1)
+                                           : replay_shuffle_t<false, false>(e, nullptr, m - 1));
+#else
     const int j = mt_randbelow_seq<uint16_t>(e, m - 1, m - 1, nullptr);  // first Fisher-Yates step picks the last slot
-    // (replay_shuffle_t<TOP14, SWAP = false>, the chunked path without swaps, measured slower here: k_resetdone 0.077 ->
-    // 0.091 ms per step at C3)
     if (m - 2 >= 1) mt_randbelow_seq<uint16_t>(e, m - 2, 1, nullptr);  // remaining draws of shuffle(empty_positions)
+#endif
     int k = 0, cell = -1;
     const int npos = S->s.n_positions[a];
     if (npos > 0) {
@@ -2568,13 +2706,30 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     }
     OT* out_a = PK ? nullptr : out_env + (size_t)a * S->obs_agent_stride;
     const int nl = S->s.n_layers[a];
+    // the agent's layer records, lane l = layer l (read per layer with v_readlane: no scalar load waited on
+    // inside the placement loop); unit tags < 16 bits, flags above them
+    uint32_t lr_tf = 0, lr_alo = 0, lr_ahi = 0;
+    {
+      const MfgLayerRec CS* lr = (const MfgLayerRec CS*)S->lrec + (size_t)a * S->lmax;
+      if (lane < nl) {
+        lr_tf = (lr[lane].unit_tags & 0xFFFFu) | (lr[lane].flags << 16);
+        lr_alo = (uint32_t)lr[lane].agent_bits;
+        lr_ahi = (uint32_t)(lr[lane].agent_bits >> 32);
+      }
+    }
     // packed mode: entry count so far and the projection accumulators (lane j holds outputs j, 64 + j, ...)
-    int pcount = 0, nq = 0;  // entries so far; entries queued for the projection
+    int qbase = 0, nq = 0;  // entries flushed so far; entries in the queue
     float acc[MFG_MAX_EMB / MFG_WAVE];
-    // project the queued entries in queue (= (block, layer, cell)) order: acc[j] += val_t * wt[idx_t][j]
+    // flush the queued entries (in (block, layer, cell) order): the stored row slots qbase + t < cap (one
+    // coalesced store per array instead of one partial store per layer block), then the projection
+    // acc[j] += val_t * wt[idx_t][j]
     auto flush = [&]() {
       const int qi = (int)pq[lane], qv = (int)pq[MFG_WAVE + lane];  // lane t holds entry t
-      for (int t = 0; t < nq; t += 4) {
+      if (pk.idx && lane < nq && qbase + lane < pk.cap) {
+        pk.idx[(size_t)a * pk.cap + qbase + lane] = (uint16_t)qi;
+        pk.val[(size_t)a * pk.cap + qbase + lane] = __int_as_float(qv);
+      }
+      for (int t = 0; pk.emb && t < nq; t += 4) {
         float w4[4][MFG_MAX_EMB / MFG_WAVE], v4[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -2593,6 +2748,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
 #pragma unroll
             for (int q = 0; q < MFG_MAX_EMB / MFG_WAVE; q++) acc[q] = __builtin_fmaf(v4[u], w4[u][q], acc[q]);
       }
+      qbase += nq;
       nq = 0;
     };
     if constexpr (PK) {
@@ -2607,10 +2763,17 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     if (0)
 #endif
     for (int w0 = 0; w0 < dd; w0 += MFG_WAVE) {
+#if MFG_OBS_CLAMP
+      // dense: lanes past the window repeat the last window cell (its value, to its address), so the layer
+      // stores need no exec mask; packed mode keeps them out (its ballots count entries)
+      const int wi = PK ? w0 + lane : min(w0 + lane, dd - 1);
+      const bool inwin = PK ? wi < dd : true;
+#else
       const int wi = w0 + lane;
       const bool inwin = wi < dd;
-      // wi / d and wi % d through a float reciprocal (exact: wi + 0.5 is >= 0.5 / d away from a multiple
-      // of d, far above the rounding error for wi < 2^12); the tests below are branch-free, every LDS
+#endif
+      // wi / d and wi % d through a float reciprocal (exact: (wi + 0.5) / d is >= 0.5 / d away from an integer
+      // and the product's error is <= (wi + 0.5) / d * 2^-23, below that for wi < 2^22); the tests below are branch-free, every LDS
       // read has a valid clamped address and its result is masked
       const int wq = (int)(((float)wi + 0.5f) * invw), wr = wi - wq * ow;
       const int x = wx0 + wq, y = wy0 + wr;
@@ -2662,10 +2825,11 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         if (tag == MFG_TAG_MACHINES) return (double)S->s.machine_pause;  // idle forever: encoding 15 (Q18)
         return 1.0;
       };
-      const MfgLayerRec CS* lr = (const MfgLayerRec CS*)S->lrec + (size_t)a * S->lmax;
-      for (int l = 0; l < nl; l++) {
-        const uint32_t ut = lr[l].unit_tags, fl = lr[l].flags;
-        const uint64_t ab = lr[l].agent_bits;
+      OT* op = PK ? nullptr : out_a + wi;  // this lane's cell of layer l: op + l * dd (advanced per layer)
+      for (int l = 0; l < nl; l++, op += PK ? 0 : dd) {
+        const uint32_t tf = (uint32_t)rl((int)lr_tf, l);
+        const uint32_t ut = tf & 0xFFFFu, fl = tf >> 16;
+        const uint64_t ab = (uint64_t)(uint32_t)rl((int)lr_alo, l) | ((uint64_t)(uint32_t)rl((int)lr_ahi, l) << 32);
         OT out = (OT)(popc(tags & ut) + popc(amask & ab));  // a small count: exact in OT
         if (fl) {
           double val = 0.0;
@@ -2696,15 +2860,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
           const bool nz = inwin && fv != 0.0f;
           const u64 nzm = ballot(nz);
           const int base = l * dd + w0;
-          if (pk.idx) {
-            const int pos = pcount + mbcnt(nzm);
-            if (nz && pos < pk.cap) {
-              pk.idx[(size_t)a * pk.cap + pos] = (uint16_t)(base + lane);
-              pk.val[(size_t)a * pk.cap + pos] = fv;
-            }
-          }
-          pcount += popc(nzm);
-          if (pk.emb && nzm) {
+          if (nzm) {
             const int nb = popc(nzm);
             if (nq + nb > MFG_WAVE) {
               wave_sync();
@@ -2725,19 +2881,20 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         // Packing rows into aligned 64-lane stores (ds_bpermute) cut that to 1.14x but cost 67 VGPRs
         // and k_obs 0.494 -> 0.543 ms, so it was dropped (k_obs).
 #if defined(MFG_ABLATE_OB_NOSTORE)  // timing only: the values are computed, (almost) never stored
-        if (inwin && out == (OT)-12345.0) out_a[(size_t)l * dd + wi] = out;
+        if (inwin && out == (OT)-12345.0) *op = out;
 #elif MFG_OBS_NT
-        if (inwin) __builtin_nontemporal_store(out, &out_a[(size_t)l * dd + wi]);
+        if (inwin) __builtin_nontemporal_store(out, op);
 #else
-        if (inwin) out_a[(size_t)l * dd + wi] = out;
+        if (inwin) *op = out;
 #endif
       }
     }
     if constexpr (PK) {
-      if (pk.emb && nq) {
+      if (nq) {
         wave_sync();
         flush();
       }
+      const int pcount = qbase;
       if (pk.idx)  // unused slots: idx 0 / val 0 (a fixed-width gather over the row stays exact)
         for (int i = pcount + lane; i < pk.cap; i += MFG_WAVE) {
           pk.idx[(size_t)a * pk.cap + i] = 0;
@@ -2946,11 +3103,11 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   if (full) {
     env_full(S, slice, e, env);
   } else {
-    e.S = S; e.lds = slice; e.scratch = (int*)(slice + ((S->L.o_mt + 15) & ~15)); e.stab = nullptr; e.cmap = nullptr;
+    e.S = S; e.lds = slice; e.scratch = (int*)(slice + S->L.o_logic); e.stab = nullptr; e.cmap = nullptr;
     e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
   }
   uint8_t* rec = state + (size_t)env * S->L.size;
-  const int bytes = full ? S->L.size : S->L.o_mt;
+  const int bytes = full ? S->L.size : S->L.o_logic;
   // lean records of <= 1 KiB: each lane keeps its 16-B chunk and writes it back only if the step changed it
   // (most of the record is per-episode constant: frozen origins, ids, counters of idle rules)
   const bool one_pass = !full && (bytes >> 4) <= MFG_WAVE;
@@ -3068,7 +3225,7 @@ __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* 
 // on the engine's second stream; null = none). With auto-reset, mfg_step renders the envs that did not finish
 // on the caller's stream while the finished ones are reset and rendered beside it.
 template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
-static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 && !PK ? 7 : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
+static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 ? (PK ? MFG_PK_WPE : 7) : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                       OT* obs, ObsPacked pk, const uint8_t* skip) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
@@ -3175,6 +3332,86 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_replay(const MfgDevSpec
   if (env >= B) return;
   if (order) env = uni(order[env]);
   replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
+}
+#endif
+
+// Two-wave replay of one env (workgroup of 128 threads; slice = the 1-wave slice + the chunk ring): wave 0
+// produces the draws, wave 1 applies the swap blocks (rp2_produce / rp2_consume). Needs the ordered exchange.
+__device__ void replay_env2(SpecP S, uint8_t* slice, uint8_t* rec) {
+  const int wv = uni(threadIdx.x >> 6);
+  const int debt = uni(((const int*)(rec + S->L.o_hdr))[H_DEBT]);
+  if (debt == 0) return;  // uniform over the workgroup
+  Env e;
+  e.S = S;
+  e.lds = slice - S->L.o_mt + 4 * RP_HDR_N;
+  e.lane = lane_id();
+  e.scratch = (int*)(slice + S->replay_sink_off);
+  e.cmap = nullptr;
+  e.stab = (uint32_t*)(slice + S->replay_stab_off);
+  e.hdrp = (int*)slice;
+  uint8_t* ring = slice + S->lds_replay_per_wave;
+  int* ctl = (int*)(ring + 2 * RP2_R * RP2_REC);  // [0], [1]: chunks in each half; [2]: the producer's last phase
+  const int t = wv * MFG_WAVE + e.lane;
+  const int n16 = S->replay_mtperm >> 4;
+  if (t < RP_HDR_N) e.hdrp[t] = ((const int*)(rec + S->L.o_hdr))[t];
+  {
+    const uint4* src = (const uint4*)(rec + S->L.o_mt);
+    uint4* dst = (uint4*)(e.lds + S->L.o_mt);
+    for (int i = t; i < n16; i += 2 * MFG_WAVE) dst[i] = src[i];
+  }
+  for (int i = t; i < S->replay_stab_n; i += 2 * MFG_WAVE) e.stab[i] = 0u;
+  if (t == 0) ctl[2] = -1;
+  __syncthreads();
+  const int hi = S->nf - 1;
+  Rp2Prod st;
+  st.s = 0;
+  st.icur = hi;
+  st.idx = e.H(H_MT_IDX);
+  st.yw = (wv == 0 && st.idx <= 560) ? e.mt()[st.idx + e.lane] : 0u;
+  uint32_t ctr = 0;
+  for (int phase = 0;; phase++) {
+    uint8_t* half = ring + (phase & 1) * RP2_R * RP2_REC;
+    if (wv == 0) {
+      if (st.s < debt) {
+        if (S->replay_top14) rp2_produce<true>(e, half, &ctl[phase & 1], st, debt, hi);
+        else rp2_produce<false>(e, half, &ctl[phase & 1], st, debt, hi);
+        if (st.s >= debt && e.lane == 0) ctl[2] = phase;
+      }
+    } else if (phase > 0) {
+      const uint8_t* prev = ring + ((phase - 1) & 1) * RP2_R * RP2_REC;
+      rp2_consume(e, prev, uni(ctl[(phase - 1) & 1]), ctr);
+    }
+    __syncthreads();
+    const int last = uni(ctl[2]);
+    if (last >= 0 && phase > last) break;  // the consumer has applied the producer's last half
+  }
+  if (wv == 0) {
+    int idx = st.idx;
+    if (idx > 624) {  // words of the next state were consumed: make the state canonical (CPython's mti)
+      mt_twist(e);
+      idx -= 624;
+    }
+    if (e.lane == 0) {
+      ((int*)(rec + S->L.o_hdr))[H_DEBT] = 0;
+      ((int*)(rec + S->L.o_hdr))[H_MT_IDX] = idx;
+    }
+  }
+  __syncthreads();
+  {
+    const uint4* src = (const uint4*)(e.lds + S->L.o_mt);
+    uint4* dst = (uint4*)(rec + S->L.o_mt);
+    for (int i = t; i < n16; i += 2 * MFG_WAVE) dst[i] = src[i];
+  }
+}
+#ifndef MFG_OBS_UNIT
+static __global__ void __launch_bounds__(2 * MFG_WAVE) k_replay2(const MfgDevSpec* S_, uint8_t* state, long long B,
+                                                                 const int* order) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  long long env = blockIdx.x;
+  if (env >= B) return;
+  if (order) env = uni(order[env]);
+  replay_env2(S, smem, state + (size_t)env * S->L.size);
 }
 #endif
 

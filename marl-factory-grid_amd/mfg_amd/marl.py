@@ -21,9 +21,9 @@ What is different from the reference, and why:
     fixture produced by the reference (tests/golden/marl_a2c.npz, tools/gen_golden_marl.py).
   * Episodes end per env (auto-reset): an entry whose previous step was done starts a new episode, so its
     action input is -1 (padding) and the recurrent state restarts from zero, as the reference does at every
-    ``env.reset()`` (``base_ac.py:98-100``). The reference's GRU runs the window in one ``nn.GRU`` call;
-    here the same parameters run as GEMMs step by step (input gates for all steps in one GEMM) so the
-    restart can happen inside a window (identical when no episode starts in it, up to f32 rounding).
+    ``env.reset()`` (``base_ac.py:98-100``). The reference's GRU runs the window in one ``nn.GRU`` call; here
+    too: every row's episode segments become sequences of one packed batch (``_Segments``), so a restart
+    inside the window costs no extra launches. Acting (one step) uses the fused ``torch.gru_cell``.
 """
 import numpy as np
 import torch
@@ -97,24 +97,77 @@ class RecurrentAC(nn.Module):
         mixed = self.mix(x_t)
         ha = hidden_actor[:, 0]
         hc = hidden_critic[:, 0]
-        keep = None if starts is None else (~starts).to(mixed.dtype)  # [N, T]
-        # the GRU input projections of all T steps as one GEMM each, then the recurrence step by step
-        # (nn.GRU semantics, torch's gate order r, z, n); plain GEMMs instead of the library RNN kernel
-        gi_a = F.linear(mixed, self.gru_actor.weight_ih_l0, self.gru_actor.bias_ih_l0)
-        gi_c = F.linear(mixed, self.gru_critic.weight_ih_l0, self.gru_critic.bias_ih_l0)
-        ps, cs = [], []
-        for s in range(t):
-            if keep is not None:
-                ha = ha * keep[:, s:s + 1]
-                hc = hc * keep[:, s:s + 1]
-            ha = _gru_cell(gi_a[:, s], ha, self.gru_actor)
-            hc = _gru_cell(gi_c[:, s], hc, self.gru_critic)
-            ps.append(ha)
-            cs.append(hc)
-        out_p, out_c = torch.stack(ps, 1), torch.stack(cs, 1)
+        if t == 1 and (starts is None or not bool(starts.any())):  # acting: one fused cell per GRU
+            out_p = torch.gru_cell(mixed[:, 0], ha, self.gru_actor.weight_ih_l0, self.gru_actor.weight_hh_l0,
+                                   self.gru_actor.bias_ih_l0, self.gru_actor.bias_hh_l0)[:, None]
+            out_c = torch.gru_cell(mixed[:, 0], hc, self.gru_critic.weight_ih_l0, self.gru_critic.weight_hh_l0,
+                                   self.gru_critic.bias_ih_l0, self.gru_critic.bias_hh_l0)[:, None]
+        elif _GRU_WINDOW == 'segments':  # a window: one library RNN call per GRU over the episode segments
+            seg = _Segments(starts, n, t, mixed.device)
+            out_p = seg.run(self.gru_actor, mixed, ha)
+            out_c = seg.run(self.gru_critic, mixed, hc)
+        else:  # a window: input gates of all steps as one GEMM, then the fused cell step by step
+            keep = None if starts is None else (~starts).to(mixed.dtype)  # [N, T]
+            ps, cs = [], []
+            for s in range(t):
+                if keep is not None:
+                    ha = ha * keep[:, s:s + 1]
+                    hc = hc * keep[:, s:s + 1]
+                ha = torch.gru_cell(mixed[:, s], ha, self.gru_actor.weight_ih_l0, self.gru_actor.weight_hh_l0,
+                                    self.gru_actor.bias_ih_l0, self.gru_actor.bias_hh_l0)
+                hc = torch.gru_cell(mixed[:, s], hc, self.gru_critic.weight_ih_l0, self.gru_critic.weight_hh_l0,
+                                    self.gru_critic.bias_ih_l0, self.gru_critic.bias_hh_l0)
+                ps.append(ha)
+                cs.append(hc)
+            out_p, out_c = torch.stack(ps, 1), torch.stack(cs, 1)
         logits = self.action_head(out_p)
         critic = self.critic_head(out_c).squeeze(-1)
         return dict(logits=logits, critic=critic, hidden_actor=out_p, hidden_critic=out_c)
+
+
+import os as _os
+_GRU_WINDOW = _os.environ.get('MFG_GRU_WINDOW', 'cells')  # 'cells' (fused cell per step) or 'segments'
+
+
+class _Segments:
+    """The episode segments of a window: row r restarts its recurrent state from zero at every entry s with
+    starts[r, s] (an episode start inside the window, base_ac.py:98-100 resets at env.reset()). Every segment
+    becomes one sequence of a packed batch (its initial state: the row's carried state, or zero after a
+    restart), so nn.GRU runs the whole window in one library call (MIOpen) instead of T cell steps, and the
+    outputs are scattered back to [N, T, H]. One host synchronisation (the segment count) per window."""
+
+    def __init__(self, starts, n, t, device):
+        st = torch.zeros((n, t), dtype=torch.bool, device=device) if starts is None else starts.clone()
+        st[:, 0] = True
+        pos = st.nonzero()  # [S, 2] (row, start), rows ascending, starts ascending within a row
+        self.rows, a = pos[:, 0], pos[:, 1]
+        s_n = pos.shape[0]
+        nxt = torch.full((s_n,), t, dtype=torch.long, device=device)
+        if s_n > 1:
+            same = self.rows[1:] == self.rows[:-1]
+            nxt[:-1] = torch.where(same, a[1:], torch.full_like(a[1:], t))
+        self.len = nxt - a  # >= 1
+        k = torch.arange(t, device=device)
+        self.valid = k[None, :] < self.len[:, None]  # [S, T]
+        self.src = (self.rows[:, None] * t + (a[:, None] + k[None, :]).clamp(max=t - 1))  # flat (row, time)
+        # the carried state only for a row's first segment, unless the row restarts at entry 0 too
+        self.first = (a == 0) if starts is None else (a == 0) & ~starts[self.rows, 0]
+        self.n, self.t = n, t
+        self.len_cpu = self.len.cpu()
+
+    def run(self, gru, x, h0):
+        from torch.nn.utils.rnn import pack_padded_sequence, pad_packed_sequence
+        n, t = self.n, self.t
+        xf = x.reshape(n * t, -1)
+        xs = xf[self.src] * self.valid[..., None].to(x.dtype)  # [S, T, I]
+        hs = torch.where(self.first[:, None], h0[self.rows], torch.zeros_like(h0[self.rows]))
+        packed = pack_padded_sequence(xs, self.len_cpu, batch_first=True, enforce_sorted=False)
+        out, _ = gru(packed, hs[None].contiguous())
+        out, _ = pad_packed_sequence(out, batch_first=True, total_length=t)  # [S, T, H]
+        dst = self.src[self.valid]
+        res = torch.zeros((n * t, out.shape[-1]), dtype=out.dtype, device=out.device)
+        res = res.index_copy(0, dst, out[self.valid])
+        return res.view(n, t, -1)
 
 
 class _PackedProj(torch.autograd.Function):

@@ -187,3 +187,31 @@ def test_batched_a2c_trains_on_device():
     e1 = tr.net.project_packed(tr.pobs.idx[1], tr.pobs.val[1])
     assert torch.allclose(e1, tr.pobs.emb[1], rtol=1e-5, atol=1e-5)
     f.close()
+
+
+def test_windowed_gru_segments_match_the_step_loop():
+    """One packed nn.GRU call over each row's episode segments == the step-by-step recurrence with the state
+    zeroed at every restart (outputs and gradients, f32 tolerance)."""
+    import torch
+    from mfg_amd.marl import _Segments, _gru_cell
+    torch.manual_seed(0)
+    n, t, i, h = 37, 6, 20, 16
+    gru = torch.nn.GRU(i, h, batch_first=True)
+    x = torch.randn(n, t, i, requires_grad=True)
+    h0 = torch.randn(n, h)
+    starts = torch.rand(n, t) < 0.2
+    starts[:, 0] = False
+    starts[3] = True  # every entry restarts
+    out = _Segments(starts, n, t, x.device).run(gru, x, h0)
+    gi = torch.nn.functional.linear(x, gru.weight_ih_l0, gru.bias_ih_l0)
+    hs, ref = h0, []
+    for s in range(t):
+        hs = hs * (~starts[:, s:s + 1]).float()
+        hs = _gru_cell(gi[:, s], hs, gru)
+        ref.append(hs)
+    ref = torch.stack(ref, 1)
+    assert torch.allclose(out, ref, atol=1e-5, rtol=1e-5)
+    g1 = torch.autograd.grad(out.square().sum(), [x, gru.weight_hh_l0])
+    g2 = torch.autograd.grad(ref.square().sum(), [x, gru.weight_hh_l0])
+    for a, b in zip(g1, g2):
+        assert torch.allclose(a, b, atol=1e-4, rtol=1e-4)
