@@ -37,8 +37,14 @@ class RecurrentAC(nn.Module):
     step-wise recurrent pass with episode restarts."""
 
     def __init__(self, observation_size, n_actions, obs_emb_size, action_emb_size, hidden_size_actor,
-                 hidden_size_critic, n_agents, use_agent_embedding=True):
+                 hidden_size_critic, n_agents, use_agent_embedding=True, gru_window='cells'):
         super().__init__()
+        # how a window of T > 1 steps runs the GRUs: 'cells' = torch.gru_cell (one fused kernel) per step,
+        # 'segments' = one nn.GRU call over packed episode segments (_Segments). Measured on the MI355X (C3,
+        # B = 8,192, n_steps 5): 32.7 vs 102.3 ms per update (MIOpen's packed-sequence GRU), so 'cells'
+        if gru_window not in ('cells', 'segments'):
+            raise ValueError("gru_window must be 'cells' or 'segments'")
+        self.gru_window = gru_window
         observation_size = int(np.prod(observation_size))
         self.n_layers = 1
         self.n_actions = n_actions
@@ -102,7 +108,7 @@ class RecurrentAC(nn.Module):
                                    self.gru_actor.bias_ih_l0, self.gru_actor.bias_hh_l0)[:, None]
             out_c = torch.gru_cell(mixed[:, 0], hc, self.gru_critic.weight_ih_l0, self.gru_critic.weight_hh_l0,
                                    self.gru_critic.bias_ih_l0, self.gru_critic.bias_hh_l0)[:, None]
-        elif _GRU_WINDOW == 'segments':  # a window: one library RNN call per GRU over the episode segments
+        elif self.gru_window == 'segments':  # a window: one library RNN call per GRU over the episode segments
             seg = _Segments(starts, n, t, mixed.device)
             out_p = seg.run(self.gru_actor, mixed, ha)
             out_c = seg.run(self.gru_critic, mixed, hc)
@@ -123,10 +129,6 @@ class RecurrentAC(nn.Module):
         logits = self.action_head(out_p)
         critic = self.critic_head(out_c).squeeze(-1)
         return dict(logits=logits, critic=critic, hidden_actor=out_p, hidden_critic=out_c)
-
-
-import os as _os
-_GRU_WINDOW = _os.environ.get('MFG_GRU_WINDOW', 'cells')  # 'cells' (fused cell per step) or 'segments'
 
 
 class _Segments:
