@@ -296,7 +296,9 @@ int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int 
  * An action index outside [0, n_actions[a]) crashes that env (MFG_CRASH_ACTION, done = 1).
  * auto_reset != 0: an env whose step is done is reset before its obs row is rendered, so the row is the
  * new episode's first observation. Per step the engine launches k_logic, k_resetdone (auto_reset) and
- * k_obs (obs != NULL); pending floor-shuffle debt is replayed (mfg_replay) once before returning. */
+ * k_obs (obs != NULL); pending floor-shuffle debt is replayed (mfg_replay) once before returning (every step
+ * on specs with long resets and an in-step floor-order consumer). Work on the engine's second stream is
+ * joined back to `stream` before the call returns. */
 int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
              int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
              uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream);
@@ -304,7 +306,9 @@ int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed,
 /* Replay pending membership-only floor shuffles (check_pos_validity, states.py:259-270, Q3). */
 int mfg_replay(mfg_engine* e, void* stream);
 
-/* Per-env state record layout (offsets) for host-side decoding; returns the number of ints written. */
+/* Per-env state record layout (offsets) for host-side decoding, then the engine's launch facts (LDS slices,
+ * o_logic, reset_overlap: 1 when a step's resets and their render run on the engine's second stream beside the
+ * render of the other envs); returns the number of ints written (<= 64). */
 int mfg_layout(const mfg_engine* e, int32_t* out);
 void* mfg_state_ptr(mfg_engine* e);
 int64_t mfg_state_bytes(const mfg_engine* e);

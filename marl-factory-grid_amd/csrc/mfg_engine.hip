@@ -33,8 +33,6 @@ struct mfg_engine {
   bool replay_each = false; // pay the shuffle debt after every step, not once per call (long resets + in-step RNG)
   int obs_nwv = 1;          // waves per env of the render (> 1: multi-wave render, k_obs_mw)
   bool replay2 = false;     // two-wave replay (k_replay2) for floor lists whose 1-wave slice fills a SIMD
-  hipStream_t ov_stream = nullptr;  // MFG_ABLATE_OVERLAP measurement only (timing of a replay overlapped with the next call)
-  hipEvent_t ov_ev = nullptr;
   struct Mark { int k; hipEvent_t a, b; };
   std::vector<Mark> marks;
   std::string err;  // mfg_last_error(e)
@@ -728,14 +726,13 @@ extern "C" int mfg_destroy(mfg_engine* e) {
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->aux) (void)hipStreamDestroy(e->aux);
-  if (e->ov_stream) (void)hipStreamDestroy(e->ov_stream);
-  if (e->ov_ev) (void)hipEventDestroy(e->ov_ev);
   delete e;
   return 0;
 }
 
 // record layout for host-side decoding (tests, snapshots):
-// [size, o_hdr, ..., o_perm, lmax, obs_agent_stride, lds_full, xchg_ordered, o_machines, ..., scratch_bytes]
+// [size, o_hdr, ..., o_perm, lmax, obs_agent_stride, lds_full, xchg_ordered, o_machines, ..., scratch_bytes, o_logic,
+//  reset_overlap (1: with auto-reset and obs, a step's resets and their render run on the engine's second stream)]
 extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
   const MfgLayout& L = e->h.L;
   const int32_t v[] = {L.size, L.o_hdr, L.o_rule_ctr, L.o_agent_pos, L.o_agent_arr, L.o_agent_par, L.o_frozen_org,
@@ -744,7 +741,7 @@ extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
                        e->h.lmax, e->h.obs_agent_stride, e->h.lds_full, e->h.xchg_ordered, L.o_machines,
                        L.o_maints, L.o_mstate, L.o_mpath, L.o_grank, e->h.dirt_cap, e->h.lds_logic, e->h.lds_obs,
                        e->h.lds_replay_per_wave, e->h.bfs_off, e->h.bfs_bytes, e->h.max_pairs, e->h.scratch_bytes,
-                       L.o_logic};
+                       L.o_logic, e->overlap ? 1 : 0};
   const int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
@@ -981,6 +978,11 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     // caller's stream renders every other env (k_logic's rd_flag tells k_obs which to leave out): a step's
     // resets are a few hundred latency-bound waves (C4: ~2.4 ms) that the full render hides.
     const bool split = e->overlap && auto_reset && obs_k;
+    // The call's replay (the shuffle debt of all K steps) after the last step's resets, on the second stream
+    // beside the last render: it touches the MT state, the permutation and two header words the render never
+    // reads, and the render's record copy is read-only (its one store, H_OVERFLOW, is another word). The
+    // render then fills the replay's drain (its longest-debt tail) instead of queueing behind it.
+    const bool replay_side = MFG_REPLAY_SIDE && k == K - 1 && obs_k;
     hipStream_t rs = split ? e->aux : st;
     if (split) {
       HIPCHK(hipEventRecord(e->ev_fork, st));
@@ -1002,27 +1004,22 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     if (split) {
       const int32_t* lst = e->h.rd_list + (size_t)rd_cur * (size_t)(e->B + 2);
       if (launch_obs(e, obs_k, obs_dtype, rs, k, nullptr, lst, MFG_K_OBS_DONE)) return -1;
+    } else if (replay_side) {  // the resets ran on the caller's stream: fork after them
+      HIPCHK(hipEventRecord(e->ev_fork, st));
+      HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
+    }
+    if (replay_side && replay_impl(e, e->aux)) return -1;
+    if (split) {
       if (launch_obs(e, obs_k, obs_dtype, st, k, e->h.rd_flag, nullptr, MFG_K_OBS)) return -1;
-      HIPCHK(hipEventRecord(e->ev_join, rs));
-      HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
     } else if (obs_k && launch_obs(e, obs_k, obs_dtype, st, k)) {
       return -1;
     }
-  }
-#ifdef MFG_ABLATE_OVERLAP
-  // timing-only build (results NOT exact: the replay races the next call's k_logic header write-back and
-  // k_resetdone; run with auto_reset = 0): the call's replay runs on a second stream, overlapped with the
-  // next call's kernels, to price a pipelined replay. Never part of the product library.
-  {
-    if (!e->ov_stream) {
-      HIPCHK(hipStreamCreateWithFlags(&e->ov_stream, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&e->ov_ev, hipEventDisableTiming));
+    if (split || replay_side) {
+      HIPCHK(hipEventRecord(e->ev_join, e->aux));
+      HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
     }
-    HIPCHK(hipEventRecord(e->ov_ev, st));
-    HIPCHK(hipStreamWaitEvent(e->ov_stream, e->ov_ev, 0));
-    return replay_impl(e, e->ov_stream);
+    if (replay_side) return 0;
   }
-#endif
   return replay_impl(e, stream);
 }
 

@@ -22,6 +22,7 @@
 //   MFG_REPLAY_EACH_STEP   pay the shuffle debt after every step (default: only for specs with long resets and an
 //                          in-step floor-order consumer); exact
 //   MFG_ABLATE_*           timing-only ablations, results NOT exact (tools/build_ablation.sh)
+//   (other MFG_* switches below select between exact variants for A/B timing)
 #ifndef MFG_NO_RAY_STATIC
 #define MFG_NO_RAY_STATIC 0
 #endif
@@ -30,6 +31,11 @@
 // 0 never, 1 when the reset is long (agents x floor cells >= 16384: the per-agent floor shuffles and draws of
 // SpawnAgents, C4/C5), 2 always
 #define MFG_RESET_OVERLAP 1
+#endif
+#ifndef MFG_REPLAY_SIDE
+// mfg_step: the call's replay on the second stream beside the last step's render. Measured neutral (C3 34.42/34.70
+// vs 34.72/34.57M env-steps/s, C4 8.94 vs 8.92M) and it blurs the per-kernel times, so it is off by default.
+#define MFG_REPLAY_SIDE 0
 #endif
 #ifndef MFG_RESET_DRAWS
 #define MFG_RESET_DRAWS 1  // SpawnAgents' shuffle(empty_positions) draws on replay_shuffle_t (0: mt_randbelow_seq)
@@ -418,6 +424,16 @@ static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice")
 #ifndef RP_SERIAL_FWD
 #define RP_SERIAL_FWD 4  // blocks with at most this many forwards resolve them serially (no LDS table)
 #endif
+// The chunk's acceptance fixed point: from the seed m, iterate m = ballot(mbcnt(m) <= c) until it is stable;
+// returns A = mbcnt(m) (#accepted lanes below this one) and leaves the accepted set in m.
+__device__ __forceinline__ int accept_ranks(u64& m, int c) {
+  for (;;) {
+    const int A = mbcnt(m);
+    const u64 m2 = ballot(A <= c);
+    if (m2 == m) return A;
+    m = m2;
+  }
+}
 // TOP14: every width k = bitlen(i + 1) is <= 14 (nf < 16384), so r = y >> (32 - k) reads only bits
 // 18..31 of the tempered word, which the last tempering step (y ^= y >> 18) leaves unchanged.
 // SWAP = false: the draws of a shuffle of hi + 1 elements only (randbelow(i + 1) for i = hi .. 1, no
@@ -471,17 +487,7 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
     // (A_l <= l, so c_l >= l accepts for sure)
     u64 m = ballot(c >= lane);
-#ifdef MFG_ABLATE_NOJACOBI
-    m = ballot(mbcnt(ballot(c >= 0)) <= c);
-    if (0)
-#endif
-    int A;
-    for (;;) {
-      A = mbcnt(m);
-      const u64 m2 = ballot(A <= c);
-      if (m2 == m) break;
-      m = m2;
-    }
+    const int A = accept_ranks(m, c);
     const int consumed = popc(ballot(A <= span));
     const int nacc = popc(m);
     const int inext = icur - nacc, idxn = idx + consumed;
@@ -632,13 +638,7 @@ __device__ void rp2_produce(const Env& e, uint8_t* half, int* cnt, Rp2Prod& st, 
     const uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
     u64 m = ballot(c >= lane);
-    int A;
-    for (;;) {
-      A = mbcnt(m);
-      const u64 m2 = ballot(A <= c);
-      if (m2 == m) break;
-      m = m2;
-    }
+    const int A = accept_ranks(m, c);
     const int consumed = popc(ballot(A <= span));
     const int nacc = popc(m);
     uint8_t* rec = half + n * RP2_REC;

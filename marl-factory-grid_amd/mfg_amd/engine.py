@@ -21,7 +21,8 @@ LAYOUT_KEYS = ['size', 'o_hdr', 'o_rule_ctr', 'o_agent_pos', 'o_agent_arr', 'o_a
                'o_frozen_gp', 'o_door', 'o_items', 'o_pods', 'o_drops', 'o_dests', 'o_dirt_pos', 'o_dirt_id',
                'o_battery', 'o_frozen_bat', 'o_dirt_amt', 'o_pcg', 'o_mt', 'o_perm', 'lmax', 'obs_agent_stride',
                'lds_full', 'xchg_ordered', 'o_machines', 'o_maints', 'o_mstate', 'o_mpath', 'o_grank', 'dirt_cap',
-               'lds_logic', 'lds_obs', 'lds_replay', 'bfs_off', 'bfs_bytes', 'max_pairs', 'scratch_bytes', 'o_logic']
+               'lds_logic', 'lds_obs', 'lds_replay', 'bfs_off', 'bfs_bytes', 'max_pairs', 'scratch_bytes', 'o_logic',
+               'reset_overlap']
 # header slots (csrc/mfg_device.h)
 HDR = {k: i for i, k in enumerate([
     'step', 'episode', 'crashed', 'frozen', 'obs_init', 'debt', 'mt_idx', 'n_items', 'n_pods', 'n_drops',
