@@ -313,7 +313,7 @@ def main():
     ap.add_argument('--alt-steps', type=int, default=None,
                     help='steps of the second measurement with the other obs dtype (default: --steps; 0 = off)')
     ap.add_argument('--packed-steps', type=int, default=None,
-                    help='steps of the packed-obs + fused-projection measurement (default: --steps; 0 = off)')
+                    help='steps of each packed-obs measurement (entries; entries + fused projection; dense + GEMM) (default: --steps; 0 = off)')
     ap.add_argument('--cap', type=int, default=32, help='packed entries stored per agent row')
     ap.add_argument('--emb', type=int, default=96, help='fused projection width (obs_emb_size of RecurrentAC)')
     ap.add_argument('--backend', default='nccl', help="torch.distributed backend for N > 1 ('nccl' = RCCL)")
@@ -437,20 +437,29 @@ def main():
                "pipeline_GBs": round(alt_value / world * alt_step_bytes / 1e9, 2),
                "pipeline_frac": round(alt_value / world * alt_step_bytes / 1e9 / HBM_PEAK_GBS, 5)}
         del obs_alt
-    # packed obs + fused policy-input projection: no dense obs at all
+    # packed obs: the nonzero entries per agent row instead of the dense obs; beside it the same
+    # with the policy-input projection fused into the render, and what that replaces (dense obs + one GEMM)
     packed = None
     packed_steps = args.steps if args.packed_steps is None else args.packed_steps
     if packed_steps > 0:
         from mfg_amd.engine import PackedObs
         kdim = eng.lmax * eng.obs_hw[0] * eng.obs_hw[1]
+        dense_bytes = core_bytes(spec) + sum(spec.n_layers) * spec.obs_hw[0] * spec.obs_hw[1] * 4
+        pe = PackedObs(eng, K=F, cap=args.cap)
+        el5 = timed(packed_steps, pe)
+        ev = B * world * packed_steps / el5
+        pe_bytes = core_bytes(spec) + A * (4 + 6 * args.cap)
+        max_nnz = int(pe.count.max())
+        del pe
         g = torch.Generator(device=dev).manual_seed(0)
         w = torch.randn((args.emb, kdim), generator=g, device=dev) * 0.05
         po = PackedObs(eng, K=F, cap=args.cap, weight=w, bias=torch.zeros(args.emb, device=dev))
         el3 = timed(packed_steps, po)
-        pk_bytes = core_bytes(spec) + A * (4 + 6 * args.cap + 4 * args.emb)
+        pk_bytes = pe_bytes + A * 4 * args.emb
         pv = B * world * packed_steps / el3
-        # what packed replaces: dense f32 obs + the policy's obs_proj over them (one GEMM per call on the same
-        # stream, hipBLASLt), i.e. the policy input from materialised obs
+        del po
+        # what the fused projection replaces: dense f32 obs + the policy's obs_proj over them (one GEMM per call on
+        # the same stream, hipBLASLt), i.e. the policy input from materialised obs
         emb_d = torch.empty((F * B * A, args.emb), device=dev)
         wt = w.t().contiguous()
 
@@ -459,16 +468,16 @@ def main():
         el4 = timed(packed_steps, None, after=proj)
         dv = B * world * packed_steps / el4
         del emb_d
-        packed = {"obs": f"packed (cap {args.cap}) + fused obs_proj (E {args.emb}, f32)", "value": round(pv, 1),
+        packed = {"obs": f"packed entries (cap {args.cap}: u16 index + f32 value per nonzero, i32 count)",
+                  "value": round(ev, 1), "unit": "env-steps/s", "steps": packed_steps,
+                  "ms_per_step": round(el5 / packed_steps * 1e3, 4), "algo_bytes_per_env_step": pe_bytes,
+                  "pipeline_GBs": round(ev / world * pe_bytes / 1e9, 2), "max_row_nnz": max_nnz,
+                  "dense_f32_bytes_per_env_step": dense_bytes,
+                  "fused_proj": {"obs": f"packed entries + fused obs_proj (E {args.emb}, f32)", "value": round(pv, 1),
+                                 "ms_per_step": round(el3 / packed_steps * 1e3, 4), "algo_bytes_per_env_step": pk_bytes,
+                                 "pipeline_GBs": round(pv / world * pk_bytes / 1e9, 2)},
                   "dense_f32_plus_proj": {"value": round(dv, 1), "ms_per_step": round(el4 / packed_steps * 1e3, 4),
-                                          "what": "dense f32 obs, then obs_proj as one f32 GEMM per call"},
-                  "unit": "env-steps/s", "steps": packed_steps, "ms_per_step": round(el3 / packed_steps * 1e3, 4),
-                  "algo_bytes_per_env_step": pk_bytes,
-                  "pipeline_GBs": round(pv / world * pk_bytes / 1e9, 2),
-                  "max_row_nnz": int(po.count.max()),
-                  "dense_f32_bytes_per_env_step": core_bytes(spec) + sum(spec.n_layers) * spec.obs_hw[0] *
-                  spec.obs_hw[1] * 4}
-        del po
+                                          "what": "dense f32 obs, then obs_proj as one f32 GEMM per call"}}
     if rank == 0:
         full = [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls if k == F] or \
                [(s.elapsed_time(e) * 1e-3, k) for s, e, k in calls]

@@ -2,6 +2,12 @@
 // include/mfg.h, launch shapes, spec upload). Device code: mfg_kernels.h; the observation-render instantiations:
 // mfg_obs_*.hip.
 #include "mfg_kernels.h"
+#ifndef MFG_REPLAY_WPB
+#define MFG_REPLAY_WPB 1  // waves per workgroup of k_replay (compile-time measurement switch)
+#endif
+#ifndef MFG_REPLAY_LPT
+#define MFG_REPLAY_LPT 1  // k_replay envs in longest-debt-first order (0: blockIdx order)
+#endif
 
 // ================================================================================================
 // host side: C-ABI (include/mfg.h)
@@ -754,16 +760,21 @@ static int wpb_for(size_t lds) { return (int)std::max<size_t>(1, std::min<size_t
 static unsigned env_grid(const mfg_engine* e, int wpb) { return (unsigned)((e->B + wpb - 1) / wpb); }
 // launch geometry of a kernel with `lds` bytes of dynamic LDS per wave
 #define GEOM(lds) dim3(env_grid(e, wpb_for(lds))), dim3(wpb_for(lds) * 64), (size_t)(lds) * wpb_for(lds)
-// waves per workgroup of k_logic / k_obs (overrides for measurements: MFG_LOGIC_WPB, MFG_OBS_WPB). k_logic runs
+// waves per workgroup of k_logic / k_obs (compile-time measurement switches MFG_LOGIC_WPB, MFG_OBS_WPB). k_logic runs
 // one wave per workgroup (C3: 0.1544 -> 0.1507 ms; its slot frees as soon as its env is done); k_obs keeps 4
-// (1 and 2 measured within noise, tools/wpb_sweep.sh)
-static int wpb_env(const char* name, int dflt) { const char* v = getenv(name); return v ? std::max(1, atoi(v)) : dflt; }
-static const int obs_wpb = wpb_env("MFG_OBS_WPB", MFG_WPB), logic_wpb = wpb_env("MFG_LOGIC_WPB", 1);
+// (1 and 2 measured within noise in round 2)
+#ifndef MFG_OBS_WPB
+#define MFG_OBS_WPB MFG_WPB
+#endif
+#ifndef MFG_LOGIC_WPB
+#define MFG_LOGIC_WPB 1
+#endif
+static const int obs_wpb = std::max(1, MFG_OBS_WPB), logic_wpb = std::max(1, MFG_LOGIC_WPB);
 #define GEOMW(lds, W) dim3(env_grid(e, std::min(W, wpb_for(lds)))), dim3(std::min(W, wpb_for(lds)) * 64), \
     (size_t)(lds) * std::min(W, wpb_for(lds))
 
 // the render kernels are instantiated in mfg_obs_*.hip (launch_obs_inst, mfg_kernels.h)
-template <int MP, typename OT, bool PK>
+template <int MP, typename OT, int PK>
 static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipStream_t st, const uint8_t* skip,
                                const int32_t* list) {
   ObsLaunch L;
@@ -834,11 +845,13 @@ static int launch_obs(mfg_engine* e, void* obs, int obs_dtype, hipStream_t st, i
   ObsPacked none{};
   if (obs_dtype == MFG_OBS_PACKED) {
     const ObsPacked pk = packed_rows(e, (const mfg_packed_obs*)obs, k);
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, true>(e, (float*)nullptr, pk, st, skip, list)));
+    // entries only (no projection registers: the render keeps its ray prefetch) or entries + fused obs_proj
+    if (pk.emb) DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, 2>(e, (float*)nullptr, pk, st, skip, list)))
+    else DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, 1>(e, (float*)nullptr, pk, st, skip, list)))
   } else if (obs_dtype == MFG_OBS_F64) {
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double, false>(e, (double*)obs, none, st, skip, list)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, double, 0>(e, (double*)obs, none, st, skip, list)));
   } else {
-    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, false>(e, (float*)obs, none, st, skip, list)));
+    DISPATCH_MP(e->maxpts, err = (launch_obs_t<MP, float, 0>(e, (float*)obs, none, st, skip, list)));
   }
   if (err != hipSuccess) return fail(std::string("k_obs launch: ") + hipGetErrorString(err));
   PROF_END(e, st, kid);
@@ -876,11 +889,10 @@ static int replay_impl(mfg_engine* e, void* stream) {
   PROF_BEGIN(e, st);
   // one wave per workgroup: a workgroup's slot is held until its slowest env's debt is paid and debts differ
   // per env, so single-wave workgroups free each slot as soon as its env is done (C3: 11.17 -> 10.91 ms per
-  // K=8 launch against 4 waves per workgroup; MFG_REPLAY_WPB overrides it for measurements)
-  static const int rwpb = [] { const char* v = getenv("MFG_REPLAY_WPB"); return v ? atoi(v) : 1; }();
-  const int wpb = std::max(1, std::min(rwpb, wpb_for(e->h.lds_replay_per_wave)));
-  // longest debt first (C3: 10.95 -> 10.47 ms per K=8 launch, the order kernels included); MFG_REPLAY_LPT=0 off
-  static const int lpt = [] { const char* v = getenv("MFG_REPLAY_LPT"); return v ? atoi(v) : 1; }();
+  // K=8 launch against 4 waves per workgroup; -DMFG_REPLAY_WPB=W builds the comparison)
+  const int wpb = std::max(1, std::min(MFG_REPLAY_WPB, wpb_for(e->h.lds_replay_per_wave)));
+  // longest debt first (C3: 10.95 -> 10.47 ms per K=8 launch, the order kernels included); -DMFG_REPLAY_LPT=0 off
+  constexpr int lpt = MFG_REPLAY_LPT;
   const unsigned g256 = (unsigned)((e->B + 255) / 256);
   if (lpt) {
     HIPCHK(hipMemsetAsync(e->rp_hist, 0, 4 * RP_NB, st));

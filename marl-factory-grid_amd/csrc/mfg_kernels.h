@@ -43,6 +43,10 @@
 #ifndef MFG_PK_WPE
 #define MFG_PK_WPE 7  // waves per SIMD asked of the short-ray packed render (1: no request)
 #endif
+#ifndef MFG_PK1_HOIST
+#define MFG_PK1_HOIST 0  // packed entries without the projection: load the first ray pass once per render (1) or per
+                         // agent (0; measured 33.86 vs 33.66M env-steps/s)
+#endif
 #ifndef MFG_OBS_CLAMP
 #define MFG_OBS_CLAMP 1  // k_obs dense placement: lanes past the window duplicate the last cell (no store masks)
 #endif
@@ -2485,7 +2489,7 @@ struct ObsPacked {
 // MW: the env's workgroup has nwv waves (wave wv renders agents wv, wv + nwv, ...); they share the lean record,
 // the cell map and the identifier pairs, each has its own per-agent tables after the shared part
 // (S->lds_obs_shared + wv * S->lds_obs_wave)
-template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT, bool MW>
+template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT, bool MW>
 __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPacked& pk, int wv, int nwv) {
   SpecP S = e.S;
   // window: oh x ow cells from (wx0, wy0) = agent - r, or the whole level at (0, 0) when pomdp_r == 0
@@ -2549,9 +2553,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
 #ifdef MFG_NO_RAY_HOIST  // measurement build: rays loaded per agent, ray words still prefetched
   constexpr bool HOIST_RAYS = false;
 #else
-  constexpr bool HOIST_RAYS = MAXPTS <= 8 && !PK;
+  constexpr bool HOIST_RAYS = MAXPTS <= 8 && (PK == 0 || (PK == 1 && MFG_PK1_HOIST));
 #endif
-  constexpr bool PREFETCH_RS = MAXPTS <= 8 && !PK;
+  constexpr bool PREFETCH_RS = MAXPTS <= 8 && PK != 2;
   RayLane<MAXPTS> ray0;
   if constexpr (HOIST_RAYS) ray0.load(S, lane);
   // ... and their static light-blocking words are fetched one agent ahead (an L2 round trip behind a
@@ -2729,7 +2733,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         pk.idx[(size_t)a * pk.cap + qbase + lane] = (uint16_t)qi;
         pk.val[(size_t)a * pk.cap + qbase + lane] = __int_as_float(qv);
       }
-      for (int t = 0; pk.emb && t < nq; t += 4) {
+      for (int t = 0; PK == 2 && pk.emb && t < nq; t += 4) {
         float w4[4][MFG_MAX_EMB / MFG_WAVE], v4[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -2751,7 +2755,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       qbase += nq;
       nq = 0;
     };
-    if constexpr (PK) {
+    if constexpr (PK == 2) {
 #pragma unroll
       for (int q = 0; q < MFG_MAX_EMB / MFG_WAVE; q++) {
         const int j = q * MFG_WAVE + lane;
@@ -2901,7 +2905,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
           pk.val[(size_t)a * pk.cap + i] = 0.0f;
         }
       if (pk.cnt && lane == 0) pk.cnt[a] = pcount;
-      if (pk.emb) {
+      if (PK == 2 && pk.emb) {
 #pragma unroll
         for (int q = 0; q < MFG_MAX_EMB / MFG_WAVE; q++) {
           const int j = q * MFG_WAVE + lane;
@@ -3187,7 +3191,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevS
 // Observation render of every env into obs[env] (read-only on the state). MM: the spec has machines or
 // maintainers (their tags, identifiers and dedupe); compiled out otherwise to keep the VGPR budget.
 // One env's render (observation_builder.py:138-235) in its LDS slice.
-template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT, bool MW = false>
+template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT, bool MW = false>
 __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* state, long long env, OT* obs,
                                         ObsPacked pk, int wv = 0, int nwv = 1) {
   // slice: [lean record][cell map][pairs] (+ per-wave tables, build_obs)
@@ -3224,8 +3228,8 @@ __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* 
 // Render of every env (skip: envs k_logic put on this step's done list, rendered by k_obs_list after their reset
 // on the engine's second stream; null = none). With auto-reset, mfg_step renders the envs that did not finish
 // on the caller's stream while the finished ones are reset and rendered beside it.
-template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
-static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 ? (PK ? MFG_PK_WPE : 7) : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
+template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT>
+static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 ? (PK == 2 ? MFG_PK_WPE : 7) : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                       OT* obs, ObsPacked pk, const uint8_t* skip) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
@@ -3237,7 +3241,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_wav
 }
 // Multi-wave render: one env per workgroup of nwv waves (specs whose per-env render slice is large, C5: a
 // 128 x 128 u16 cell map; the waves share it and split the agents)
-template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
+template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT>
 static __global__ void __launch_bounds__(8 * 64) k_obs_mw(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                            OT* obs, ObsPacked pk, const uint8_t* skip) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -3246,7 +3250,7 @@ static __global__ void __launch_bounds__(8 * 64) k_obs_mw(const MfgDevSpec* S_, 
   if (env >= B || (skip && skip[env])) return;  // uniform over the workgroup
   obs_env<MAXPTS, OT, MM, PK, DIRT, true>(S, smem, state, env, obs, pk, uni(threadIdx.x >> 6), blockDim.x >> 6);
 }
-template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
+template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT>
 static __global__ void __launch_bounds__(8 * 64) k_obs_mw_list(const MfgDevSpec* S_, const uint8_t* state,
                                                                 long long B, OT* obs, ObsPacked pk,
                                                                 const int32_t* list) {
@@ -3260,7 +3264,7 @@ static __global__ void __launch_bounds__(8 * 64) k_obs_mw_list(const MfgDevSpec*
   }
 }
 // Render of the envs of a done list (rd_list row: [0] = count, [2..] = envs): a resident grid strides over it.
-template <int MAXPTS, typename OT, bool MM, bool PK, bool DIRT>
+template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT>
 static __global__ void __launch_bounds__(MFG_WPB * 64) k_obs_list(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                            OT* obs, ObsPacked pk, const int32_t* list) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -3529,11 +3533,11 @@ struct ObsLaunch {
 };
 // k_obs over every env (list = null; skip: flags of envs left to a list render) or over a done list (a resident
 // grid striding over it)
-template <int MP, typename OT, bool PK>
+template <int MP, typename OT, int PK>
 hipError_t launch_obs_inst(const ObsLaunch& L, OT* obs, const ObsPacked& pk, hipStream_t st, const uint8_t* skip,
                            const int32_t* list);
 #define MFG_DEFINE_LAUNCH_OBS                                                                                    \
-  template <int MP, typename OT, bool PK>                                                                        \
+  template <int MP, typename OT, int PK>                                                                        \
   hipError_t launch_obs_inst(const ObsLaunch& L, OT* obs, const ObsPacked& pk, hipStream_t st,                   \
                              const uint8_t* skip, const int32_t* list) {                                        \
     MFG_OBS_LAUNCH_IF(true, true) else MFG_OBS_LAUNCH_IF(true, false) else MFG_OBS_LAUNCH_IF(false, true)          \
@@ -3563,11 +3567,13 @@ hipError_t launch_obs_inst(const ObsLaunch& L, OT* obs, const ObsPacked& pk, hip
                            L.d_state, L.B, obs, pk, skip);                                                       \
     }                                                                                                            \
   }
-// explicit instantiations of one ray length (the three obs modes: packed, f64, f32)
+// explicit instantiations of one ray length (the obs modes: packed + fused projection, packed entries only, f64, f32)
 #define MFG_INSTANTIATE_OBS(MP)                                                                                  \
-  template hipError_t launch_obs_inst<MP, float, true>(const ObsLaunch&, float*, const ObsPacked&, hipStream_t,   \
-                                                       const uint8_t*, const int32_t*);                          \
-  template hipError_t launch_obs_inst<MP, double, false>(const ObsLaunch&, double*, const ObsPacked&,            \
-                                                         hipStream_t, const uint8_t*, const int32_t*);           \
-  template hipError_t launch_obs_inst<MP, float, false>(const ObsLaunch&, float*, const ObsPacked&, hipStream_t, \
-                                                        const uint8_t*, const int32_t*);
+  template hipError_t launch_obs_inst<MP, float, 2>(const ObsLaunch&, float*, const ObsPacked&, hipStream_t,      \
+                                                    const uint8_t*, const int32_t*);                             \
+  template hipError_t launch_obs_inst<MP, float, 1>(const ObsLaunch&, float*, const ObsPacked&, hipStream_t,      \
+                                                    const uint8_t*, const int32_t*);                             \
+  template hipError_t launch_obs_inst<MP, double, 0>(const ObsLaunch&, double*, const ObsPacked&, hipStream_t,    \
+                                                     const uint8_t*, const int32_t*);                            \
+  template hipError_t launch_obs_inst<MP, float, 0>(const ObsLaunch&, float*, const ObsPacked&, hipStream_t,      \
+                                                    const uint8_t*, const int32_t*);

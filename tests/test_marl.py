@@ -110,16 +110,16 @@ def test_stepwise_restarts():
 # ---------------------------------------------------------------------------------------------------------
 # GPU: the engine's packed mode
 # ---------------------------------------------------------------------------------------------------------
-def _engine_pair(cfg, B, K, E=96, cap=64, seed_base=0):
+def _engine_pair(cfg, B, K, E=96, cap=64, seed_base=0, proj=True):
     from mfg_amd.spec import compile_spec
     from mfg_amd.engine import Engine, PackedObs
     spec = compile_spec(cfg)
     dense, packed = Engine(spec, B, device=0), Engine(spec, B, device=0)
     kdim = dense.lmax * dense.obs_hw[0] * dense.obs_hw[1]
     g = torch.Generator().manual_seed(1)
-    w = (torch.randn(E, kdim, generator=g) * 0.1).cuda()
-    b = (torch.randn(E, generator=g) * 0.1).cuda()
-    po = PackedObs(packed, K=K, cap=cap, weight=w, bias=b)
+    w = (torch.randn(E, kdim, generator=g) * 0.1).cuda() if proj else None
+    b = (torch.randn(E, generator=g) * 0.1).cuda() if proj else None
+    po = PackedObs(packed, K=K, cap=cap, weight=w, bias=b)  # no weight: the entries-only render
     return spec, dense, packed, po, w, b
 
 
@@ -130,6 +130,8 @@ def _check_rows(dense_obs, po, w, b, k):
     nnz = (flat != 0).sum(-1).to(torch.int32)
     assert torch.equal(po.count[k], nnz)
     assert torch.equal(po.dense(k).reshape(B, A, -1), flat)
+    if w is None:
+        return
     ref = flat.double() @ w.double().t() + b.double()
     err = (po.emb[k].double() - ref).abs()
     tol = 1e-5 * (flat.double().abs() @ w.double().abs().t() + b.double().abs()) + 1e-6
@@ -137,10 +139,12 @@ def _check_rows(dense_obs, po, w, b, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('cfg,B,K', [('large8.yaml', 2048, 8), ('rooms4.yaml', 512, 4), ('alltest16.yaml', 96, 2),
-                                     ('simple1.yaml', 256, 4)])
-def test_packed_obs_matches_dense(cfg, B, K):
-    spec, dense, packed, po, w, b = _engine_pair(cfg, B, K)
+@pytest.mark.parametrize('cfg,B,K,proj', [('large8.yaml', 2048, 8, True), ('rooms4.yaml', 512, 4, True),
+                                          ('alltest16.yaml', 96, 2, True), ('simple1.yaml', 256, 4, True),
+                                          ('large8.yaml', 2048, 8, False), ('alltest16.yaml', 96, 2, False),
+                                          ('grid128_64.yaml', 8, 2, False)])
+def test_packed_obs_matches_dense(cfg, B, K, proj):
+    spec, dense, packed, po, w, b = _engine_pair(cfg, B, K, proj=proj, cap=1024 if 'grid128' in cfg else 64)
     obs = torch.zeros(dense.obs_shape(K), dtype=torch.float32, device='cuda')
     dense.reset(obs=obs[0], init=True, seed_base=5)
     packed.reset(obs=po.view(0), init=True, seed_base=5)
