@@ -43,6 +43,12 @@
 #ifndef MFG_PK_WPE
 #define MFG_PK_WPE 7  // waves per SIMD asked of the short-ray packed render (1: no request)
 #endif
+#ifndef MFG_RESET_INLINE
+#define MFG_RESET_INLINE 1  // env_reset inlined into the reset kernels; k_resetdone asks 4 waves per SIMD (<= 128 VGPRs)
+#endif
+#ifndef MFG_RPD_QUEUE
+#define MFG_RPD_QUEUE 1  // k_replay_done takes done envs from a work queue (0: fixed stride over the list)
+#endif
 #ifndef MFG_PK1_HOIST
 #define MFG_PK1_HOIST 0  // packed entries without the projection: load the first ray pass once per render (1) or per
                          // agent (0; measured 33.86 vs 33.66M env-steps/s)
@@ -2013,7 +2019,11 @@ __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
 // ------------------------------------------------------------------------------------------------
 // reset (factory.py:134-148; global_entities.py:196-203; rules.py:182-199; SpawnEntity rules)
 // ------------------------------------------------------------------------------------------------
+#if MFG_RESET_INLINE  // inlined into k_reset / k_resetdone, so their register budget (waves_per_eu) applies to it
+__device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scratch) {
+#else
 __device__ void env_reset(const Env& e, int* scratch) {
+#endif
   SpecP S = e.S;
   const int A = S->A, W = S->s.W;
   int reset_crash = 0;  // a reference exception inside reset(): reported by the next step (crashed + done)
@@ -3144,8 +3154,9 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     int32_t* lst = S->rd_list + (size_t)rd_slot * (size_t)(B + 2);
     if (e.lane == 0) lst[2 + atomicAdd(&lst[0], 1)] = (int32_t)env;
   }
-  // the next step's list is empty: its last reader (the previous step's k_resetdone) has finished
-  if (blockIdx.x == 0 && threadIdx.x == 0) S->rd_list[(size_t)(rd_slot ^ 1) * (size_t)(B + 2)] = 0;
+  // the next step's list is empty ([0] count, [1] k_replay_done's taken counter): its last reader (the previous
+  // step's k_resetdone) has finished
+  if (blockIdx.x == 0 && threadIdx.x < 2) S->rd_list[(size_t)(rd_slot ^ 1) * (size_t)(B + 2) + threadIdx.x] = 0;
   wave_sync();
   if (one_pass) {
     if (e.lane < (bytes >> 4)) {
@@ -3162,8 +3173,8 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
 // Factory.reset(). A fixed grid of waves strides over the list (count <= B, every wave exits), so a step
 // with few episode ends costs a few waves instead of one wave per env.
 #ifndef MFG_OBS_UNIT  // host-unit kernel (not compiled in the render units)
-static __global__ void __launch_bounds__(MFG_WPB * 64) k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B,
-                                                            int rd_slot) {
+static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MFG_RESET_INLINE ? 4 : 1)))
+k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B, int rd_slot) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const int wid = uni(threadIdx.x >> 6);  // wave-uniform: slice and record addresses become scalar
@@ -3508,12 +3519,30 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_replay_done(const MfgDe
   const int wid = uni(threadIdx.x >> 6);
   const int32_t* lst = S->rd_list + (size_t)rd_slot * (size_t)(B + 2);
   const long long n = min((long long)uni(lst[0]), B);
+#if MFG_RPD_QUEUE
+  // each wave's first env is its own index; after that the waves take entries nw, nw + 1, ... from a work queue
+  // (lst[1] counts the entries taken, k_logic zeroes it with the count): debts differ per env, so a wave takes
+  // its next env when it is done instead of a fixed stride. A step with few episode ends touches the counter
+  // only from the waves that had an env; every wave exits once its index passes n.
+  int* taken = S->rd_list + (size_t)rd_slot * (size_t)(B + 2) + 1;
+  const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+  long long q = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
+  while (q < n) {
+    const long long env = uni(lst[2 + q]);
+    if (env >= 0 && env < B)
+      replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
+    int t = 0;
+    if (__lane_id() == 0) t = atomicAdd(taken, 1);
+    q = nw + rl(t, 0);
+  }
+#else
   const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
   for (long long q = (long long)blockIdx.x * (blockDim.x >> 6) + wid; q < n; q += nw) {
     const long long env = uni(lst[2 + q]);
     if (env < 0 || env >= B) continue;
     replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
   }
+#endif
 }
 #endif
 

@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B timing of exact engine variants: tools/ab_run.sh VARIANT... (build/ablate/libmfg_hip_VARIANT.so, built by
-# tools/build_ablation.sh with -DMFG_<VARIANT>) against the in-tree library, alternating, 2 rounds each.
+# A/B timing of engine variants: tools/ab_run.sh VARIANT... (build/ablate/libmfg_hip_VARIANT.so, built by
+# tools/build_variant.sh or tools/build_ablation.sh) against the in-tree library, alternating, 2 rounds each.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 for r in 1 2; do
