@@ -590,7 +590,11 @@ def main():
                                    f"pomdp_r 3" if args.config == 'large8.yaml' else Path(args.config).stem,
                        "envs_per_gpu": B, "global_batch": B * world,
                        "obs": f"dense {args.obs_dtype} per env-step ({obs_bytes} B)",
-                       "fuse": F, "auto_reset": True, "parallelism": f"env-shard x{world}"},
+                       "fuse": F, "auto_reset": True, "parallelism": f"env-shard x{world}",
+                       "window": f"steps {args.warmup}..{args.warmup + args.steps} of every env" + (
+                           "" if args.warmup + args.steps > 500 or args.config != 'large8.yaml' else
+                           " (inside the first 500-step episode: no reset and no episode-2 obs path timed; the "
+                           "default --warmup 600 --steps 2000 window times 4 episode ends)")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "alt_obs_dtype": alt,

@@ -186,13 +186,36 @@ class _PackedProj(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         idx, val = ctx.saved_tensors
-        gw = torch.zeros((ctx.k, g.shape[1]), dtype=g.dtype, device=g.device)
-        step = max(1, (1 << 27) // max(ctx.k, 1))  # dense row blocks of <= 512 MiB
-        for r0 in range(0, idx.shape[0], step):
-            d = torch.zeros((min(step, idx.shape[0] - r0), ctx.k), dtype=g.dtype, device=g.device)
-            d.scatter_add_(1, idx[r0:r0 + step], val[r0:r0 + step].to(g.dtype))
-            gw.addmm_(d.t(), g[r0:r0 + step])
-        return None, None, gw
+        return None, None, _packed_weight_grad(idx, val, g, ctx.k)
+
+
+def _packed_weight_grad(idx, val, g, k):
+    """D^T @ g for the packed rows (idx, val) [M, cap] scattered to dense D [M, k]: one GEMM per block of rows
+    (<= 512 MiB of dense rows), instead of embedding_bag's M x cap x E atomics onto the k x E table."""
+    gw = torch.zeros((k, g.shape[1]), dtype=g.dtype, device=g.device)
+    step = max(1, (1 << 27) // max(k, 1))
+    for r0 in range(0, idx.shape[0], step):
+        d = torch.zeros((min(step, idx.shape[0] - r0), k), dtype=g.dtype, device=g.device)
+        d.scatter_add_(1, idx[r0:r0 + step], val[r0:r0 + step].to(g.dtype))
+        gw.addmm_(d.t(), g[r0:r0 + step])
+    return gw
+
+
+class _EngineProj(torch.autograd.Function):
+    """obs_proj(obs) for the learner, forward taken from the engine: every slot of the window was rendered with
+    the current weights (the fused projection of k_obs, MFG_OBS_PACKED), so the forward is that output (bias
+    included) and only the backward touches the packed rows (weight: D^T g, bias: the row sum of g)."""
+
+    @staticmethod
+    def forward(ctx, idx, val, weight, bias, emb):
+        ctx.save_for_backward(idx, val)
+        ctx.k = weight.shape[1]
+        return emb.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, val = ctx.saved_tensors
+        return None, None, _packed_weight_grad(idx, val, g, ctx.k).t(), g.sum(0), None
 
 
 def _gru_cell(gi, h, gru):
@@ -239,13 +262,15 @@ class BatchedA2C:
 
     Per step: the engine renders o_t as packed rows + the fused ``obs_proj`` (one kernel, no dense obs); the
     policy acts on (o_t, a_{t-1}, h_t); actions go straight back into ``mfg_step`` (int32 on the device).
-    Every ``n_steps`` steps: one A2C update on the window o_0..o_T (``base_ac.py:126-128``), with obs_proj
-    re-evaluated by ``embedding_bag`` over the stored entries. No host synchronisation inside ``step``;
+    Every ``n_steps`` steps: one A2C update on the window o_0..o_T (``base_ac.py:126-128``). obs_proj's forward is
+    the render's own fused output (every slot was rendered with the current weights; ``engine_emb=False``
+    re-evaluates it by ``embedding_bag`` over the stored entries), its backward runs on the stored entries. No host
+    synchronisation inside ``step``;
     ``learn`` syncs once when ``check_cap`` is set (truncated packed rows raise)."""
 
     def __init__(self, factory, net=None, n_steps=5, gamma=0.99, entropy_coef=0.01, vf_coef=0.5, gae_coef=0.0,
                  lr=3e-4, cap=32, obs_emb_size=96, action_emb_size=16, hidden_size=64, use_agent_embedding=False,
-                 check_cap=True, generator=None):
+                 check_cap=True, generator=None, engine_emb=True):
         from .engine import PackedObs
         self.f = factory
         eng = factory.engine
@@ -272,6 +297,7 @@ class BatchedA2C:
         self.T, self.gamma, self.entropy_coef, self.vf_coef, self.gae_coef = n_steps, gamma, entropy_coef, \
             vf_coef, gae_coef
         self.check_cap = check_cap
+        self.engine_emb = engine_emb  # learner forward of obs_proj: the engine's fused output (True) or a gather
         self.gen = generator
         T, N, dev = self.T, self.N, self.dev
         # obs slots o_0..o_T of the window (entries + fused projection), written by the engine
@@ -342,15 +368,26 @@ class BatchedA2C:
         rew = self.rew.permute(1, 2, 0).reshape(N, T).to(torch.float32)
         return idx, val, a_in, acts, starts, rew, d
 
+    def loss(self):
+        """The A2C loss of the current window (base_ac.py:200-217), with grad."""
+        idx, val, a_in, acts, starts, rew, d = self.window()
+        with torch.enable_grad():
+            if self.engine_emb:  # the forward from the render's fused projection (same weights), no gather
+                T, N, cap = self.T, self.N, idx.shape[-1]
+                emb_pre = self.pobs.emb.permute(1, 2, 0, 3).reshape(N * (T + 1), -1)
+                emb = _EngineProj.apply(idx.reshape(-1, cap).long(), val.reshape(-1, cap), self.net.obs_proj.weight,
+                                        self.net.obs_proj.bias, emb_pre).view(N, T + 1, -1)
+            else:
+                emb = self.net.project_packed(idx, val)
+            out = self.net.forward_emb(emb, a_in, self.h0a, self.h0c, agent_ids=self.agent_ids, starts=starts)
+            return a2c_loss(out, acts, rew, d, self.gamma, self.entropy_coef, self.vf_coef, self.gae_coef)
+
     def learn(self):
         """One A2C update on the window (base_ac.py:200-225), then slide: o_T becomes o_0."""
         if self.check_cap:
             self.pobs.check()
-        idx, val, a_in, acts, starts, rew, d = self.window()
         with torch.enable_grad():
-            emb = self.net.project_packed(idx, val)
-            out = self.net.forward_emb(emb, a_in, self.h0a, self.h0c, agent_ids=self.agent_ids, starts=starts)
-            loss = a2c_loss(out, acts, rew, d, self.gamma, self.entropy_coef, self.vf_coef, self.gae_coef)
+            loss = self.loss()
             self.opt.zero_grad()
             loss.backward()
             torch.nn.utils.clip_grad_norm_(self.net.parameters(), 0.5)

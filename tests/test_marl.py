@@ -193,6 +193,32 @@ def test_batched_a2c_trains_on_device():
     f.close()
 
 
+@pytest.mark.gpu
+def test_a2c_loss_from_engine_projection_matches_gather():
+    """The learner's obs_proj forward taken from the render's fused output gives the embedding_bag loss and
+    gradients (f32 tolerance): every window slot was rendered with the current weights."""
+    from mfg_amd.factory import BatchedFactory
+    from mfg_amd.marl import BatchedA2C
+    f = BatchedFactory('large8.yaml', 256, seed_base=2)
+    tr = BatchedA2C(f, n_steps=5, generator=torch.Generator(device='cuda').manual_seed(1))
+    tr.train(2)  # weights moved away from init; o_0 re-projected by the gather
+    learn, tr.learn = tr.learn, (lambda: None)
+    for _ in range(tr.T):
+        tr.step()
+    tr.learn = learn
+    res = {}
+    for mode in (True, False):
+        tr.engine_emb = mode
+        tr.net.zero_grad()
+        loss = tr.loss()
+        loss.backward()
+        res[mode] = (float(loss), {n: p.grad.detach().clone() for n, p in tr.net.named_parameters() if p.grad is not None})
+    assert abs(res[True][0] - res[False][0]) <= 1e-5 * max(1.0, abs(res[False][0]))
+    for n, g in res[False][1].items():
+        assert torch.allclose(res[True][1][n], g, rtol=1e-3, atol=1e-6), n
+    f.close()
+
+
 def test_windowed_gru_segments_match_the_step_loop():
     """One packed nn.GRU call over each row's episode segments == the step-by-step recurrence with the state
     zeroed at every restart (outputs and gradients, f32 tolerance)."""
