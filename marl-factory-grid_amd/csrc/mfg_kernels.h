@@ -60,6 +60,10 @@
 #define MFG_RPV 3  // k_replay swap-block variant bits (exact; see replay_shuffle_t)
 #endif
 static_assert(!(MFG_RPV & 1) || (MFG_RPV & 2), "MFG_RPV bit 1 (no read sink) needs bit 2 (masked i write)");
+#ifndef MFG_RPS
+#define MFG_RPS 0  // k_replay chunk arithmetic (exact): bit 1 the width band on the VALU, bit 2 one-compare forward
+                   // test, bit 4 the i-cell address on the VALU
+#endif
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -490,10 +494,23 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
     // start the next chunk). So every chunk takes the same branch-free path, power-of-two crossings
     // and the i < 64 tail included.
-    const int sh = __clz(icur + 1);
-    const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
+#if MFG_RPS & 1
+    // the chunk's band arithmetic on a vector copy of icur: per chunk the VALU has slack and the CU's one
+    // scalar unit does not (k_replay issues ~20 SALU and ~34 VALU per chunk)
+    int icv;
+    asm("v_mov_b32 %0, %1" : "=v"(icv) : "s"(icur));
+#else
+    const int icv = icur;
+#endif
+#if MFG_RPS & 1  // icur >= lo = 1 in the loop: icur + 1 >= 2, so no zero guard on the count and no max with lo
+    const int sh = __builtin_clz((unsigned)(icv + 1));
+    const int span = icv + 1 - (int)(0x80000000u >> sh);  // highest rank at width k
+#else
+    const int sh = __clz(icv + 1);
+    const int span = icv - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
+#endif
     uint32_t r = y >> sh;
-    const int c = min(icur - (int)r, span);
+    const int c = min(icv - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
     // (A_l <= l, so c_l >= l accepts for sure)
     u64 m = ballot(c >= lane);
@@ -508,10 +525,10 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     } else {
     // (a chunk with no accepted draw runs the block on the sinks: rare, and one branch less per chunk)
     const bool acc = lanes(m);
-    const int i = icur - A, j = (int)r;
+    const int i = icv - A, j = (int)r;
     uint16_t* const ptop = perm + icur;  // wave-uniform
 #if MFG_RPV & 1  // rejected lanes read the next accepted rank's cell (same address: a broadcast, no sink bank)
-    uint16_t* pi = ptop - A;
+    uint16_t* pi = (MFG_RPS & 4) ? perm + i : ptop - A;  // RPS 4: the address on the VALU
 #else
     uint16_t* pi = acc ? ptop - A : sink;
 #endif
@@ -522,7 +539,15 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // icur - j_s (rejected lanes sharing that rank carry no swap and may take the value harmlessly).
     // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
     // and pointer jumping resolves the chains.
+#if MFG_RPS & 2
+    // j in (inext, i) as one vector compare: min(j - inext, i - j) > 0. Rejected lanes never qualify (r > i when
+    // the draw fails, i = inext for lanes past the chunk's last accepted draw), so no "& m".
+    int dmin;
+    asm("v_min_i32 %0, %1, %2" : "=v"(dmin) : "v"(j - inext), "v"(i - j));
+    u64 cm = ballot(dmin > 0);
+#else
     u64 cm = ballot(j > inext) & ballot(j < i) & m;
+#endif
 #ifdef MFG_ABLATE_NOFWD
     cm = 0;
 #endif
