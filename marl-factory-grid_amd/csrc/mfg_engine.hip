@@ -195,7 +195,7 @@ static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int
   L->o_frozen_bat = o; o += 8 * A;
   o = align_up(o, 16);
   L->o_mt = o; o += 4 * 624;
-  L->o_perm = o; o += 2 * s->n_floor;
+  L->o_perm = o; o += std::max(2 * s->n_floor, 128);  // >= 128 B after MT: mt_twist reads up to word 652 (dropped)
   o = align_up(o, 4);
   L->o_mstate = o; o += 4 * kmax * mstate_ints;
   L->o_mpath = o; o += 2 * kmax * path_cap;

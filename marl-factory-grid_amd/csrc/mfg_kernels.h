@@ -60,9 +60,12 @@
 #define MFG_RPV 3  // k_replay swap-block variant bits (exact; see replay_shuffle_t)
 #endif
 static_assert(!(MFG_RPV & 1) || (MFG_RPV & 2), "MFG_RPV bit 1 (no read sink) needs bit 2 (masked i write)");
+#ifndef MFG_TWIST
+#define MFG_TWIST 1  // MT19937 twist: phases 2/3 take mt[i - 227] from the previous phase's registers (exact)
+#endif
 #ifndef MFG_RPS
-#define MFG_RPS 0  // k_replay chunk arithmetic (exact): bit 1 the width band on the VALU, bit 2 one-compare forward
-                   // test, bit 4 the i-cell address on the VALU
+#define MFG_RPS 76  // k_replay chunk arithmetic (exact; 0 = the round-2 form): bit 4 the i-cell address from i,
+                    // bit 8 the exchange's half shift from j, bit 64 the consumed count on the SALU
 #endif
 #include <stdint.h>
 #include <stdio.h>
@@ -195,6 +198,57 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
 // 454<=i<623: mt[i-227] new). Each phase issues all its LDS reads before any of its writes, so one
 // wave pays three LDS round trips per 624 draws. (Taking mt[i+1] from the neighbour lane by DPP wave_shl
 // instead of a third LDS read was bit-exact and measured no faster: k_replay 11.05-11.12 vs 10.97-11.03 ms.)
+#if MFG_TWIST
+// The third operand of phases 2 and 3, mt[i - 227], is the previous phase's result in the same lane and slot
+// (i - 227 = i0 - 227 + t * 64 + lane), and new[623] takes old[623], new[0] and new[396] from lanes too. So no read
+// waits on a write: the 26 reads of old words are issued first, then the writes, one sync per twist (was 33
+// reads, 3 round trips and 4 syncs). Every address is one lane base plus an immediate offset: reads past a phase's
+// end fetch words of the same slice (later MT words or the permutation) whose results are dropped, and only the
+// last slot of each phase masks its writes, so no per-slot clamp or sink select runs on the VALU.
+__device__ void mt_twist(const Env& e) {
+  uint32_t* const p = e.mt() + e.lane;
+  const int lane = e.lane;
+  uint32_t a1[4], b1[4], c1[4], a2[4], b2[4], a3[3], b3[3];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    a1[t] = p[t * MFG_WAVE]; b1[t] = p[t * MFG_WAVE + 1]; c1[t] = p[t * MFG_WAVE + 397];
+  }
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    a2[t] = p[227 + t * MFG_WAVE]; b2[t] = p[227 + t * MFG_WAVE + 1];
+  }
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    a3[t] = p[454 + t * MFG_WAVE]; b3[t] = p[454 + t * MFG_WAVE + 1];
+  }
+  uint32_t v1[4], v2[4], v3[3];
+#pragma unroll
+  for (int t = 0; t < 4; t++) v1[t] = mt_mix(a1[t], b1[t], c1[t]);
+#pragma unroll
+  for (int t = 0; t < 4; t++) v2[t] = mt_mix(a2[t], b2[t], v1[t]);
+#pragma unroll
+  for (int t = 0; t < 3; t++) v3[t] = mt_mix(a3[t], b3[t], v2[t]);
+  // new[623] = mix(old[623], new[0], new[396]): old[623] is b3[2] of lane 40 (word 622 + 1), new[0] v1[0] of lane 0,
+  // new[396] v2[2] of lane 41 (396 = 227 + 128 + 41)
+  const uint32_t last = mt_mix((uint32_t)rl((int)b3[2], 40), (uint32_t)rl((int)v1[0], 0), (uint32_t)rl((int)v2[2], 41));
+  // every read before any write: per lane the read and write offsets differ, so without a fence the compiler may
+  // move a write above a read of another lane's word (e.g. lane 0's store of word 64 above lane 63's read of it)
+  wave_sync();
+#pragma unroll
+  for (int t = 0; t < 3; t++) p[t * MFG_WAVE] = v1[t];  // words 0..191
+#pragma unroll
+  for (int t = 0; t < 3; t++) p[227 + t * MFG_WAVE] = v2[t];  // 227..418
+#pragma unroll
+  for (int t = 0; t < 2; t++) p[454 + t * MFG_WAVE] = v3[t];  // 454..581
+  if (lane < 35) {  // 192..226 and 419..453
+    p[3 * MFG_WAVE] = v1[3];
+    p[227 + 3 * MFG_WAVE] = v2[3];
+  }
+  if (lane < 41) p[454 + 2 * MFG_WAVE] = v3[2];  // 582..622
+  if (lane == 0) p[623] = last;
+  wave_sync();
+}
+#else
 __device__ void mt_twist(const Env& e) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
@@ -239,6 +293,7 @@ __device__ void mt_twist(const Env& e) {
   *(lane == 0 ? &mt[623] : sink) = last;
   wave_sync();
 }
+#endif
 
 // Draw random.randbelow(i+1) for i = hi, hi-1, ..., lo (the inner loop of random.shuffle,
 // random.py:380-395 with _randbelow_with_getrandbits, random.py:239-249). 64 draws are tempered in
@@ -494,29 +549,21 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
     // start the next chunk). So every chunk takes the same branch-free path, power-of-two crossings
     // and the i < 64 tail included.
-#if MFG_RPS & 1
-    // the chunk's band arithmetic on a vector copy of icur: per chunk the VALU has slack and the CU's one
-    // scalar unit does not (k_replay issues ~20 SALU and ~34 VALU per chunk)
-    int icv;
-    asm("v_mov_b32 %0, %1" : "=v"(icv) : "s"(icur));
-#else
-    const int icv = icur;
-#endif
-#if MFG_RPS & 1  // icur >= lo = 1 in the loop: icur + 1 >= 2, so no zero guard on the count and no max with lo
-    const int sh = __builtin_clz((unsigned)(icv + 1));
-    const int span = icv + 1 - (int)(0x80000000u >> sh);  // highest rank at width k
-#else
-    const int sh = __clz(icv + 1);
-    const int span = icv - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
-#endif
+    const int sh = __clz(icur + 1);
+    const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
     uint32_t r = y >> sh;
-    const int c = min(icv - (int)r, span);
+    const int c = min(icur - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
     // (A_l <= l, so c_l >= l accepts for sure)
     u64 m = ballot(c >= lane);
     const int A = accept_ranks(m, c);
-    const int consumed = popc(ballot(A <= span));
     const int nacc = popc(m);
+#if MFG_RPS & 64  // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1),
+                  // and then exactly the lanes up to the last accepted one (scalar, no vector compare)
+    const int consumed = nacc > span ? 64 - __builtin_clzll(m) : 64;
+#else
+    const int consumed = popc(ballot(A <= span));
+#endif
     const int inext = icur - nacc, idxn = idx + consumed;
 #ifndef MFG_ABLATE_NOSWAP
     if constexpr (!SWAP) {
@@ -525,7 +572,7 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     } else {
     // (a chunk with no accepted draw runs the block on the sinks: rare, and one branch less per chunk)
     const bool acc = lanes(m);
-    const int i = icv - A, j = (int)r;
+    const int i = icur - A, j = (int)r;
     uint16_t* const ptop = perm + icur;  // wave-uniform
 #if MFG_RPV & 1  // rejected lanes read the next accepted rank's cell (same address: a broadcast, no sink bank)
     uint16_t* pi = (MFG_RPS & 4) ? perm + i : ptop - A;  // RPS 4: the address on the VALU
@@ -539,15 +586,7 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // icur - j_s (rejected lanes sharing that rank carry no swap and may take the value harmlessly).
     // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
     // and pointer jumping resolves the chains.
-#if MFG_RPS & 2
-    // j in (inext, i) as one vector compare: min(j - inext, i - j) > 0. Rejected lanes never qualify (r > i when
-    // the draw fails, i = inext for lanes past the chunk's last accepted draw), so no "& m".
-    int dmin;
-    asm("v_min_i32 %0, %1, %2" : "=v"(dmin) : "v"(j - inext), "v"(i - j));
-    u64 cm = ballot(dmin > 0);
-#else
     u64 cm = ballot(j > inext) & ballot(j < i) & m;
-#endif
 #ifdef MFG_ABLATE_NOFWD
     cm = 0;
 #endif
@@ -601,6 +640,18 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     if (acc) F = lds_xchg_u16_issue(&perm[j], (uint32_t)v);
     if (idxn <= 560) yw = mt[idxn + lane];
     F = lds_xchg_u16_wait(F, &perm[j]);
+#elif MFG_RPS & 8  // the half's shift from j: shifts read the low 5 bits, so j << 4 is (j & 1) * 16 (perm is
+                   // dword aligned in every LDS image); rejected lanes edit either half of their sink word
+    uint32_t F;
+    {
+      const uint32_t sh = (uint32_t)j << 4;
+      const uint32_t ad = (uint32_t)(uintptr_t)(acc ? &perm[j] : sink) & ~3u;
+      asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(F) : "v"(ad), "v"(0xFFFFu << (sh & 31u)),
+                   "v"((uint32_t)v << (sh & 31u)) : "memory");
+      if (idxn <= 560) yw = mt[idxn + lane];
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F) : : "memory");
+      asm("v_lshrrev_b32 %0, %1, %2" : "=v"(F) : "v"(sh), "v"(F));  // low 5 bits of sh; the i write keeps 16 bits
+    }
 #else
     uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
     if (idxn <= 560) yw = mt[idxn + lane];
