@@ -8,8 +8,9 @@ for v in "$@"; do
   echo "$v: $(tail -1 gpurun_out/bis_$v.log)"
 done
 for r in 1 2; do
-  for v in "$@"; do
-    MFG_HIP_LIB=build/ablate/libmfg_hip_$v.so timeout -k 10 200 python bench.py --no-cpu-baseline --alt-steps 0 \
+  for v in base "$@"; do
+    lib=""; [ "$v" != base ] && lib="build/ablate/libmfg_hip_$v.so"
+    MFG_HIP_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --alt-steps 0 \
       --packed-steps 0 --steps 800 --warmup 200 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
     python -c "
 import json; d=json.load(open('gpurun_out/ab_$v.json'))
