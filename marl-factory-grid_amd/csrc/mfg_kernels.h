@@ -64,8 +64,9 @@ static_assert(!(MFG_RPV & 1) || (MFG_RPV & 2), "MFG_RPV bit 1 (no read sink) nee
 #define MFG_TWIST 1  // MT19937 twist: phases 2/3 take mt[i - 227] from the previous phase's registers (exact)
 #endif
 #ifndef MFG_RPS
-#define MFG_RPS 76  // k_replay chunk arithmetic (exact; 0 = the round-2 form): bit 4 the i-cell address from i,
-                    // bit 8 the exchange's half shift from j, bit 64 the consumed count on the SALU
+#define MFG_RPS 92  // k_replay chunk arithmetic (exact; 0 = the round-2 form): bit 4 the i-cell address from i,
+                    // bit 8 the exchange's half shift from j, bit 16 the Jacobi seed at 3l/4, bit 64 the consumed
+                    // count on the SALU
 #endif
 #include <stdint.h>
 #include <stdio.h>
@@ -526,6 +527,7 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   // (idx <= 560) the raw words of the next chunk are loaded one chunk ahead, so whether this chunk's
   // words are already in yw follows from idx alone (a twisted state had idx >= 624 > 560).
   uint32_t yw = idx <= 560 ? mt[idx + lane] : 0u;
+  const int lane34 = (3 * lane) >> 2;
   while (icur >= lo) {
     if (idx > 560) {
       if (idx >= 624) {
@@ -555,7 +557,12 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     const int c = min(icur - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
     // (A_l <= l, so c_l >= l accepts for sure)
+#if MFG_RPS & 16  // seed at A_l ~ 3l/4 (the mean acceptance): 1.91 Jacobi rounds per chunk instead of 2.15 (simulated
+                  // over C3's chunks); any seed converges to the same unique fixed point (lane l is exact after l rounds)
+    u64 m = ballot(c >= lane34);
+#else
     u64 m = ballot(c >= lane);
+#endif
     const int A = accept_ranks(m, c);
     const int nacc = popc(m);
 #if MFG_RPS & 64  // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1),
@@ -723,10 +730,17 @@ __device__ void rp2_produce(const Env& e, uint8_t* half, int* cnt, Rp2Prod& st, 
     const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);
     const uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
+#if MFG_RPS & 16  // the single-wave replay's seed and consumed count (replay_shuffle_t)
+    u64 m = ballot(c >= (3 * lane) >> 2);
+    const int A = accept_ranks(m, c);
+    const int nacc = popc(m);
+    const int consumed = nacc > span ? 64 - __builtin_clzll(m) : 64;
+#else
     u64 m = ballot(c >= lane);
     const int A = accept_ranks(m, c);
     const int consumed = popc(ballot(A <= span));
     const int nacc = popc(m);
+#endif
     uint8_t* rec = half + n * RP2_REC;
     if (lanes(m)) ((uint16_t*)(rec + 4))[A] = (uint16_t)r;
     if (lane == 0) *(int*)rec = icur | (nacc << 16);
