@@ -19,7 +19,9 @@ Limits (what cannot run in or beside the kernel, rejected or documented):
   * a custom rule sees the state at the end of the device step. That equals the reference's view at its
     hook for everything the device rules do not change inside tick_step / tick_post_step (agent positions
     and states, items, dirt, destinations, batteries after their rule); door timers are updated by
-    DoorAutoClose in tick_step, so a rule placed before it sees the ticked timers;
+    DoorAutoClose in tick_step. Where that differs -- a device rule later in the step than the custom rule's
+    hook changes what it reads (`_MUTATORS`) -- the view refuses the read with `StaleStateError` instead of
+    handing out the end-of-step value;
   * custom Entities and Actions are rejected (`UnsupportedSpec`): they would change the step itself.
 """
 import dataclasses
@@ -29,8 +31,55 @@ from pathlib import Path
 
 from . import info as _info
 from . import views as _views
+from .spec import UnsupportedSpec
 
 NO_POS = (-9999, -9999)
+
+# Device rules that change state inside a step, by the hook phase they do it in (reference: doors/rules.py
+# DoorAutoClose.tick_step, maintenance/rules.py MoveMaintainers.tick_step, batteries/rules.py
+# BatteryDecharge.tick_step/tick_post_step, clean_up/rules.py RespawnDirt.tick_step and
+# EntitiesSmearDirtOnMove.tick_post_step, destinations/rules.py DestinationReachReward.tick_step,
+# items/rules.py RespawnItems.tick_step/tick_post_step, environment/rules.py WatchCollisions.tick_post_step).
+# {rule: {phase: {group: attributes changed, or None for the whole group (membership, positions)}}}
+_BATT = {'Batteries': ('charge_level', 'is_discharged')}
+_MUTATORS = {
+    'DoorAutoClose': {_info.TICK: {'Doors': ('is_open', 'is_closed', 'time_to_close')}},
+    'MoveMaintainers': {_info.TICK: {'Maintainers': None}},
+    'BatteryDecharge': {_info.TICK: _BATT, _info.POST: _BATT},
+    'DoneAtBatteryDischarge': {_info.TICK: _BATT, _info.POST: _BATT},
+    'RespawnDirt': {_info.TICK: {'DirtPiles': None}},
+    'EntitiesSmearDirtOnMove': {_info.POST: {'DirtPiles': None}},
+    'DestinationReachReward': {_info.TICK: {'Destinations': None}},
+    'DoneAtDestinationReach': {_info.TICK: {'Destinations': None}},
+    'RespawnItems': {_info.TICK: {'Items': None}, _info.POST: {'Items': None}},
+    'WatchCollisions': {_info.POST: {'Agents': ('state',)}},
+}
+
+
+class StaleStateError(UnsupportedSpec):
+    """A custom rule read state that a device rule later in the same step changes: the host view holds the
+    end-of-step value, the reference would show the value at the custom rule's hook."""
+
+
+def stale_state(spec, slot, phase):
+    """{group: attrs | None} a host rule at rule position `slot` must not read in hook `phase`, and the device
+    rule that makes each stale. The views are end-of-step snapshots (PRE: before the step), so everything a
+    device rule changes at or after (phase, slot) is ahead of the reference's state at that hook. The TICK view
+    carries the agents' action results as their states, so WatchCollisions' later states do not leak into it."""
+    if phase in (_info.PRE, _info.DONE):
+        return {}
+    out = {}
+    for i, name in enumerate(spec.rule_names):
+        for ph, groups in _MUTATORS.get(name, {}).items():
+            if ph < phase or (ph == phase and i < slot):
+                continue
+            for g, attrs in groups.items():
+                if g == 'Agents' and ph != phase:
+                    continue
+                prev = out.get(g, ((), None))[0]
+                merged = None if attrs is None or prev is None else tuple(prev) + tuple(attrs)
+                out[g] = (merged, name)
+    return out
 
 
 def locate_custom_class(name, folder):
@@ -64,10 +113,13 @@ def level_map(spec):
 class _Frozen:
     """Attribute bag that refuses assignment (host rules observe, they cannot change the device state)."""
 
-    def __init__(self, **kw):
+    def __init__(self, _stale=None, **kw):
         object.__setattr__(self, '_d', kw)
+        object.__setattr__(self, '_stale', _stale or {})
 
     def __getattr__(self, k):
+        if k in self._stale:
+            raise StaleStateError(self._stale[k])
         try:
             return self._d[k]
         except KeyError:
@@ -104,6 +156,16 @@ class GroupView(list):
 
     def __repr__(self):
         return f'{self.name}[{len(self)}]'
+
+
+def _pos_dict(groups):
+    """`entities.pos_dict` (groups/global_entities.py): entities by position, walls and agents first."""
+    pos_dict = {}
+    for g in ('Walls', 'Agents') + tuple(x for x in groups if x not in ('Walls', 'Agents', 'Batteries')):
+        for e in groups[g]:
+            if e.pos != NO_POS:
+                pos_dict.setdefault(e.pos, []).append(e)
+    return pos_dict
 
 
 class StateView:
@@ -145,15 +207,35 @@ class StateView:
                 EntityView(name=f'Battery[{a.name}]', bound_entity=a, charge_level=float(b), is_discharged=b == 0)
                 for a, b in zip(agents, snap.battery)])
         self._groups = groups
-        pos_dict = {}
-        for g in ('Walls', 'Agents') + tuple(x for x in groups if x not in ('Walls', 'Agents', 'Batteries')):
-            for e in groups[g]:
-                if e.pos != NO_POS:
-                    pos_dict.setdefault(e.pos, []).append(e)
-        self.entities = _Frozen(pos_dict=pos_dict, names=list(groups), floorlist_cells=len(spec.floor_cells))
+        self.entities = _Frozen(pos_dict=_pos_dict(groups), names=list(groups), floorlist_cells=len(spec.floor_cells))
+
+    def restricted(self, stale, who):
+        """This view with the reads in `stale` ({group: (attrs | None, device rule)}) refused for rule `who`."""
+        if not stale:
+            return self
+        v = object.__new__(StateView)
+        v.spec, v.snap, v.curr_step = self.spec, self.snap, self.curr_step
+        v._whole = {}
+        groups = dict(self._groups)
+        for g, (attrs, dev) in stale.items():
+            if g not in groups:
+                continue
+            msg = (f'custom rule {who!r} reads {g}{"" if attrs is None else "." + "/".join(attrs)}, which the '
+                   f'device rule {dev!r} changes later in the step; the host view only holds the end-of-step state')
+            if attrs is None:
+                v._whole[g] = msg
+            else:
+                groups[g] = GroupView(g, [type(e)(_stale={a: msg for a in attrs}, **e._d) for e in groups[g]])
+        v._groups = groups
+        pos_msg = next((m for g, m in v._whole.items() if g != 'Batteries'), None)
+        kw = dict(self.entities._d, pos_dict=_pos_dict(groups))
+        v.entities = _Frozen(_stale={'pos_dict': pos_msg} if pos_msg else None, **kw)
+        return v
 
     def __getitem__(self, key):
         key = {'Agent': 'Agents', 'Wall': 'Walls'}.get(key, key)
+        if key in getattr(self, '_whole', {}):
+            raise StaleStateError(self._whole[key])
         try:
             return self._groups[key]
         except KeyError:
@@ -164,7 +246,7 @@ class StateView:
 
     @property
     def moving_entites(self):  # states.py:120-122 (sic)
-        return list(self._groups['Agents'])
+        return list(self['Agents'])
 
 
 def _as_res(r, phase, slot, names):
@@ -183,6 +265,9 @@ class HostRules:
     def __init__(self, spec):
         self.spec = spec
         self.rules = [(slot, cls(**(kw or {}))) for slot, name, cls, kw in spec.host_rules]
+        self.stale = [{ph: stale_state(spec, slot, ph) for ph in (_info.TICK, _info.POST)}
+                      for slot, _, _, _ in spec.host_rules]
+        self.rule_names = [name for _, name, _, _ in spec.host_rules]
         self.names = [f'Agent[{n}]' for n in spec.agent_names]
 
     def __bool__(self):
@@ -205,8 +290,9 @@ class HostRules:
         out = []
         for phase, hook in ((_info.PRE, 'tick_pre_step'), (_info.TICK, 'tick_step'), (_info.POST, 'tick_post_step'),
                             (_info.DONE, 'on_check_done')):
-            for slot, r in self.rules:
-                for x in getattr(r, hook)(views[phase]) or []:
+            for k, (slot, r) in enumerate(self.rules):
+                view = views[phase].restricted(self.stale[k].get(phase), self.rule_names[k])
+                for x in getattr(r, hook)(view) or []:
                     out.append(_as_res(x, phase, slot - 0.5, self.names))
         return out
 

@@ -127,3 +127,61 @@ def test_builtin_name_wins_over_a_custom_class(tmp_path, compat_path):
     names = [n for _, n, _, _ in spec.host_rules]
     assert 'WatchCollisions' not in names
     assert names == ['PenaltyBeforeActions', 'CountFailedActions', 'DoorProximityBonus', 'DoneWhenCrowded']
+
+
+_READERS = '''
+from marl_factory_grid.environment.rules import Rule
+
+
+class DoorTimerReader(Rule):
+    """tick_step: reads the door timers DoorAutoClose ticks in the same hook."""
+    def tick_step(self, state):
+        return [] if sum(d.time_to_close for d in state['Doors']) < -1 else []
+
+
+class DoorPosReader(Rule):
+    """tick_step: reads only door positions (static)."""
+    def tick_step(self, state):
+        return [] if len([d.pos for d in state['Doors']]) < 0 else []
+'''
+
+
+def test_stale_reads_refused(tmp_path, compat_path):
+    """A custom rule's view is the end-of-step state; a read of state that a device rule changes later in the
+    step (host_rules._MUTATORS) raises StaleStateError instead of returning a value the reference would not
+    show. Placed after DoorAutoClose the same read is exact; door positions never change."""
+    import oracle as O
+    import yaml
+    from views_compare import oracle_snapshot
+    from mfg_amd.spec import compile_spec
+    from mfg_amd.host_rules import HostRules, StaleStateError, fold_step, pre_snapshot, stale_state
+    from mfg_amd import info as I
+    (tmp_path / 'mods').mkdir()
+    (tmp_path / 'mods' / 'readers.py').write_text(_READERS)
+    base = yaml.safe_load((ROOT / 'marl-factory-grid_amd' / 'mfg_amd' / 'configs' / CFG).read_text())
+
+    def run(rules):
+        cfg = dict(base, Rules=rules)
+        p = tmp_path / 'cfg.yaml'
+        p.write_text(yaml.safe_dump(cfg, sort_keys=False))
+        spec = compile_spec(p, custom_modules_path=str(tmp_path / 'mods'))
+        env = O.OracleEnv(spec, 0)
+        env.reset()
+        host = HostRules(spec)
+        try:
+            for _ in range(3):
+                pre = pre_snapshot(oracle_snapshot(env))
+                _, ddone, ev = env.step([0] * spec.n_agents, with_obs=False)
+                fold_step(spec, host, [0] * spec.n_agents, ev, pre, oracle_snapshot(env), ddone)
+        finally:
+            env.close()
+        return spec
+
+    close = {'DoorAutoClose': {'close_frequency': 10}}
+    spec = run({'DoorPosReader': None, **close})  # positions: never stale
+    assert [slot for slot, *_ in spec.host_rules] == [0]
+    assert stale_state(spec, 0, I.TICK)['Doors'][1] == 'DoorAutoClose'
+    assert stale_state(spec, 1, I.TICK) == {} and stale_state(spec, 0, I.DONE) == {}
+    run({**close, 'DoorTimerReader': None})  # after DoorAutoClose: the end-of-step timers are the hook's
+    with pytest.raises(StaleStateError, match='DoorAutoClose'):
+        run({'DoorTimerReader': None, **close})
