@@ -41,6 +41,9 @@ for _p in (ROOT / 'marl-factory-grid_amd', ROOT / 'oracle', ROOT / 'tests'):
         sys.path.insert(0, str(_p))
 
 ALGO_BYTES_PER_ENV_STEP = 11391  # 415 B state/IO + 10,976 B dense fp32 obs (C3); f64 obs: 22,367
+PARITY_TESTS = {  # the GPU tests that pin the exact mode each line times (tests/test_gpu_timed_path.py)
+    'f64': 'tests/test_gpu_timed_path.py::test_timed_path_k8_f64_b65536_matches_oracle',
+    'f32': 'tests/test_gpu_timed_path.py::test_timed_path_k8_fp32_b65536_matches_oracle'}
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CU_CLOCK_HZ, N_CU = 2.4e9, 256   # MI355X: 256 CUs, 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
 BOX_CPU_SHARE = 16               # host cores the GPU box allots one GPU (worker pools are sized to it)
@@ -184,12 +187,14 @@ def _free_port():
     return port
 
 
-def launch_ranks(n, argv, share_gpu=False, dry_run=False):
+def launch_ranks(n, argv, share_gpu=False, dry_run=False, rank_timeout=900.0):
     """`bench.py --gpus N` (N > 1) started without a torch.distributed launcher: run N rank processes of this
     script, one per GPU, and print rank 0's JSON line. The parent stays GPU-free: it only counts devices
     (torch.cuda.device_count() does not initialise HIP on this image) and starts each rank as a child process
     with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as torch.distributed.run would.
-    If any rank fails the others are killed (by their own Popen handles) and the largest exit code returned."""
+    If any rank fails the others are killed (by their own Popen handles) and the largest exit code returned; if
+    the ranks are still running after `rank_timeout` seconds (an RCCL init or barrier hang), all are killed and
+    124 is returned."""
     if not (share_gpu or dry_run):
         import torch
         visible = torch.cuda.device_count()
@@ -206,8 +211,18 @@ def launch_ranks(n, argv, share_gpu=False, dry_run=False):
         procs.append(subprocess.Popen([sys.executable, '-u', str(Path(__file__).resolve())] + list(argv), env=env,
                                       stdout=out if r == 0 else subprocess.DEVNULL))
     rc = 0
+    t_start = time.monotonic()
     while procs:
         time.sleep(0.2)
+        if time.monotonic() - t_start > rank_timeout:
+            print(f"bench.py: ranks still running after {rank_timeout:.0f}s, killing them", file=sys.stderr)
+            for q in procs:
+                q.kill()
+            for q in procs:
+                q.wait()
+            procs = []
+            rc = 124
+            break
         for p in list(procs):
             code = p.poll()
             if code is None:
@@ -308,8 +323,9 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--cpu-workers', type=int, default=0,
                     help='0 = min(16, affinity cores): the GPU box allots 16 host cores per GPU')
-    ap.add_argument('--obs-dtype', choices=['f32', 'f64'], default='f32',
-                    help='obs precision of the headline line (the reference returns f64 obs, Q25)')
+    ap.add_argument('--obs-dtype', choices=['f32', 'f64'], default='f64',
+                    help='obs precision of the headline line: f64, the reference\'s own (Q25, '
+                         'utils/observation_builder.py:162); f32 is the alt_obs_dtype side line')
     ap.add_argument('--alt-steps', type=int, default=None,
                     help='steps of the second measurement with the other obs dtype (default: --steps; 0 = off)')
     ap.add_argument('--packed-steps', type=int, default=None,
@@ -318,6 +334,8 @@ def main():
     ap.add_argument('--emb', type=int, default=96, help='fused projection width (obs_emb_size of RecurrentAC)')
     ap.add_argument('--backend', default='nccl', help="torch.distributed backend for N > 1 ('nccl' = RCCL)")
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--rank-timeout', type=float, default=900.0,
+                    help='bench.py --gpus N as its own launcher: kill the ranks after this many seconds')
     ap.add_argument('--no-profile', action='store_true', help='no per-kernel HIP events in the timed region')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU rehearsal of the rank protocol (gloo, no GPU, no engine); not a bench number')
@@ -325,7 +343,7 @@ def main():
 
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         return launch_ranks(args.gpus, sys.argv[1:], share_gpu=os.environ.get('MFG_BENCH_SHARE_GPU') == '1',
-                            dry_run=args.dry_run)
+                            dry_run=args.dry_run, rank_timeout=args.rank_timeout)
     world, rank, local, n_ranks = init_ranks(args)
     if args.dry_run:
         return dry_run(args, world, rank, n_ranks)
@@ -568,6 +586,20 @@ def main():
         roof["peak_measured_how"] = "device-to-device copy of 2 GiB (2 x 2 GiB moved), best of 10"
         if peak_meas and roof.get("achieved"):
             roof["frac_of_measured"] = round(roof["achieved"] / peak_meas, 5)
+        if dom:
+            # SURVEY §8(d)'s definition charged to the dominant kernel: the whole env-step's algorithmic bytes x the
+            # env-steps one launch of it covers (k_replay: B x K), over its mean launch time. `frac` above uses the
+            # kernel's own minimal bytes (MT + permutation); this is the figure the §8(d) table reads.
+            steps_per_launch = B * (k_call if dom == 'k_replay' else 1)
+            sec8d = step_bytes * steps_per_launch / (kernels[dom]["mean_launch_ms"] * 1e-3) / 1e9
+            sec8d_f32 = ALGO_BYTES_PER_ENV_STEP * steps_per_launch / (kernels[dom]["mean_launch_ms"] * 1e-3) / 1e9 \
+                if args.config == 'large8.yaml' else None
+            roof["frac_sec8d"] = round(sec8d / HBM_PEAK_GBS, 5)
+            roof["sec8d"] = {"algo_bytes_per_env_step": step_bytes, "env_steps_per_launch": steps_per_launch,
+                             "achieved_GBs": round(sec8d, 2),
+                             "frac_with_f32_obs_bytes": round(sec8d_f32 / HBM_PEAK_GBS, 5) if sec8d_f32 else None,
+                             "how": "SURVEY §8(d) bytes per env-step (this line's obs dtype; 11,391 B with f32 obs) x "
+                                    "env-steps per launch of the dominant kernel / its mean launch time / 8 TB/s"}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             visible = len(os.sched_getaffinity(0))
@@ -596,6 +628,16 @@ def main():
                            " (inside the first 500-step episode: no reset and no episode-2 obs path timed; the "
                            "default --warmup 600 --steps 2000 window times 4 episode ends)")},
             "roofline": roof,
+            "parity": {"status": "bit-exact vs the C oracle, itself pinned by reference-generated fixtures",
+                       "timed_mode_test": PARITY_TESTS[args.obs_dtype] if args.config == 'large8.yaml' else None,
+                       "timed_mode": "K=8 mfg_step calls, Philox actions, auto-reset, B=65,536, 608 steps across the "
+                                     "episode-500 reset; 256 envs vs their own oracle env every step (f64 rewards ==, "
+                                     "done, events, obs bits), MT19937 + floor order after every call",
+                       "fixture_seeds": "tests/golden/large8_s{0,1}: reference step replayed through the C-ABI "
+                                        "(tests/test_gpu_parity.py), py_seed 0 and 1",
+                       "side_lines": {"alt_obs_dtype": PARITY_TESTS['f32' if args.obs_dtype == 'f64' else 'f64'],
+                                      "packed_obs": "tests/test_marl.py (packed rows scatter to the dense f32 obs "
+                                                    "bit-exactly)"}},
             "cpu_baseline": cpu,
             "alt_obs_dtype": alt,
             "packed_obs": packed,

@@ -563,7 +563,11 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
 #else
     u64 m = ballot(c >= lane);
 #endif
+#ifdef MFG_ABLATE_NOJACOBI  // timing only: the seed taken as the accepted set (no fixed-point iteration)
+    const int A = mbcnt(m);
+#else
     const int A = accept_ranks(m, c);
+#endif
     const int nacc = popc(m);
 #if MFG_RPS & 64  // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1),
                   // and then exactly the lanes up to the last accepted one (scalar, no vector compare)

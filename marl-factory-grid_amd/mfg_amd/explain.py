@@ -52,23 +52,12 @@ def _custom_rules(folder):
     """{name: {kwarg: default or '!'}} of the Rule subclasses defined under `folder` (tools.py:43-58 explains a
     class by its and its bases' __init__ signatures). Custom Rules are the custom plugin kind this build runs
     (on the host, mfg_amd.host_rules); custom Actions and Entities are rejected by compile_spec."""
-    import importlib.util
     import inspect
-    import sys
-    folder = Path(folder).resolve()
+    from .host_rules import custom_modules
     out = {}
-    for path in sorted(folder.rglob('*.py')):
-        if '__init__' in path.name:
-            continue
-        mod_name = 'mfg_custom_' + '_'.join(path.relative_to(folder).with_suffix('').parts)
-        mod = sys.modules.get(mod_name)
-        if mod is None:
-            spec = importlib.util.spec_from_file_location(mod_name, path)
-            mod = importlib.util.module_from_spec(spec)
-            sys.modules[mod_name] = mod
-            spec.loader.exec_module(mod)
+    for mod in custom_modules(folder):
         for key, obj in vars(mod).items():
-            if key.startswith('_') or not inspect.isclass(obj) or obj.__module__ != mod_name:
+            if key.startswith('_') or not inspect.isclass(obj) or obj.__module__ != mod.__name__:
                 continue
             if not any(b.__name__ == 'Rule' for b in obj.__mro__[1:]):
                 continue

@@ -20,7 +20,7 @@ import numpy as np
 
 from . import abi
 from .engine import Engine, PackedObs, RecordView, events_from_rows, EV_MISC, HDR, HDR_N
-from .host_rules import HostRules, StateView, fold_step, level_map, pre_snapshot
+from .host_rules import HostRules, StaleStateError, StateView, fold_step, level_map, pre_snapshot
 from .info import rebuild_info
 from .spec import compile_spec, UnsupportedSpec
 from . import views as _views
@@ -89,6 +89,7 @@ class Factory:
         self._agent_states = None  # agent.state per agent after the last step (None: all Noop/valid)
         self._manual = None        # manual_* protocol: actions collected since manual_step_init
         self._last = None          # (reward, done, info) of the last executed step
+        self._stale_step = False   # a host rule's StaleStateError ended the last step: reset() before stepping
         # Factory.__init__: entities, rules, OBSBuilder (its floor-list access shuffles once, Q3)
         if self._sync:
             self._push_random()
@@ -158,6 +159,7 @@ class Factory:
         self._torch.cuda.synchronize(self._dev)
         self._agent_states = None
         self._step = 0
+        self._stale_step = False
         if self._host:
             view = StateView(self.spec, self.snapshot())
             if not self._host_init:  # rules.do_all_init (factory.py:121); the view is the reset state here
@@ -168,6 +170,9 @@ class Factory:
 
     def step(self, actions):
         """factory.py:189-220. Returns (None, obs list, reward, done, info)."""
+        if self._stale_step:
+            raise RuntimeError('a custom rule raised StaleStateError in the last step after the engine had already '
+                               'executed it; call reset() before stepping again')
         if not isinstance(actions, list):
             actions = [int(actions)]
         A = self.spec.n_agents
@@ -195,8 +200,12 @@ class Factory:
         self._step = ev['step']
         self._agent_states = _views.agent_states(self.spec, actions, ev_a, ev_w)
         if self._host:  # custom rules: their Results join the device's in rule order, then one fold
-            reward, done, info = fold_step(self.spec, self._host, [int(x) for x in actions], ev, pre,
-                                           self.snapshot(), done)
+            try:
+                reward, done, info = fold_step(self.spec, self._host, [int(x) for x in actions], ev, pre,
+                                               self.snapshot(), done)
+            except StaleStateError:
+                self._stale_step = True  # the device stepped but this step's results were never returned
+                raise
             info = dict(info)
         else:
             info = dict(rebuild_info(self.spec, [int(x) for x in actions], ev, reward))

@@ -37,39 +37,49 @@ NO_POS = (-9999, -9999)
 
 # Device rules that change state inside a step, by the hook phase they do it in (reference: doors/rules.py
 # DoorAutoClose.tick_step, maintenance/rules.py MoveMaintainers.tick_step, batteries/rules.py
-# BatteryDecharge.tick_step/tick_post_step, clean_up/rules.py RespawnDirt.tick_step and
-# EntitiesSmearDirtOnMove.tick_post_step, destinations/rules.py DestinationReachReward.tick_step,
-# items/rules.py RespawnItems.tick_step/tick_post_step, environment/rules.py WatchCollisions.tick_post_step).
+# BatteryDecharge.tick_step, clean_up/rules.py RespawnDirt.tick_step, destinations/rules.py
+# DestinationReachReward.tick_step, environment/rules.py WatchCollisions.tick_post_step).
 # {rule: {phase: {group: attributes changed, or None for the whole group (membership, positions)}}}
+# Not listed, because they change nothing a view shows: RespawnItems (never spawns, SURVEY Q9: the item count
+# stays at its limit, items/rules.py:28-43), EntitiesSmearDirtOnMove (never smears, Q1: move identifiers never
+# match is_move, clean_up/rules.py:79), the tick_post_step of BatteryDecharge / DoneAtBatteryDischarge (it only
+# paralyses agents, batteries/rules.py:66-87; charge changes in tick_step).
 _BATT = {'Batteries': ('charge_level', 'is_discharged')}
 _MUTATORS = {
     'DoorAutoClose': {_info.TICK: {'Doors': ('is_open', 'is_closed', 'time_to_close')}},
     'MoveMaintainers': {_info.TICK: {'Maintainers': None}},
-    'BatteryDecharge': {_info.TICK: _BATT, _info.POST: _BATT},
-    'DoneAtBatteryDischarge': {_info.TICK: _BATT, _info.POST: _BATT},
+    'BatteryDecharge': {_info.TICK: _BATT},
+    'DoneAtBatteryDischarge': {_info.TICK: _BATT},
     'RespawnDirt': {_info.TICK: {'DirtPiles': None}},
-    'EntitiesSmearDirtOnMove': {_info.POST: {'DirtPiles': None}},
-    'DestinationReachReward': {_info.TICK: {'Destinations': None}},
-    'DoneAtDestinationReach': {_info.TICK: {'Destinations': None}},
-    'RespawnItems': {_info.TICK: {'Items': None}, _info.POST: {'Items': None}},
+    'DestinationReachReward': {_info.TICK: {'Destinations': ('reached',)}},
+    'DoneAtDestinationReach': {_info.TICK: {'Destinations': ('reached',)}},
     'WatchCollisions': {_info.POST: {'Agents': ('state',)}},
 }
+# rules that change state only on the steps where they emit a Result: RespawnDirt on its spawn steps
+# (clean_up/rules.py:49-59), the reach rules when a destination is reached (destinations/rules.py:33-54)
+_ON_RESULT = {'RespawnDirt', 'DestinationReachReward', 'DoneAtDestinationReach'}
 
 
 class StaleStateError(UnsupportedSpec):
     """A custom rule read state that a device rule later in the same step changes: the host view holds the
-    end-of-step value, the reference would show the value at the custom rule's hook."""
+    end-of-step value, the reference would show the value at the custom rule's hook. Raised from inside
+    `Factory.step` after the device has executed the step: the Factory then refuses further steps until
+    `reset()` (the step's rewards and info were never returned)."""
 
 
-def stale_state(spec, slot, phase):
-    """{group: attrs | None} a host rule at rule position `slot` must not read in hook `phase`, and the device
-    rule that makes each stale. The views are end-of-step snapshots (PRE: before the step), so everything a
-    device rule changes at or after (phase, slot) is ahead of the reference's state at that hook. The TICK view
-    carries the agents' action results as their states, so WatchCollisions' later states do not leak into it."""
+def stale_state(spec, slot, phase, fired=None):
+    """{group: (attrs | None, device rule)} a host rule at rule position `slot` must not read in hook `phase`.
+    The views are end-of-step snapshots (PRE: before the step), so everything a device rule changes at or after
+    (phase, slot) is ahead of the reference's state at that hook. `fired`: the device rule indices that emitted a
+    Result this step (None = assume every rule fired); a rule in `_ON_RESULT` that did not fire changed nothing.
+    The TICK view carries the agents' action results as their states, so WatchCollisions' later states do not
+    leak into it."""
     if phase in (_info.PRE, _info.DONE):
         return {}
     out = {}
     for i, name in enumerate(spec.rule_names):
+        if name in _ON_RESULT and fired is not None and i not in fired:
+            continue
         for ph, groups in _MUTATORS.get(name, {}).items():
             if ph < phase or (ph == phase and i < slot):
                 continue
@@ -82,20 +92,33 @@ def stale_state(spec, slot, phase):
     return out
 
 
-def locate_custom_class(name, folder):
-    """The class `name` from the .py files under `folder` (helpers.py:215-250 searches them with rglob and
-    returns the first module that defines it). Modules are imported by file location."""
+def custom_modules(folder):
+    """The modules of the .py files under `folder` (helpers.py:215-250 searches them with rglob), imported by file
+    location, in path order. Module names carry a hash of the resolved folder, so two folders with a `rules.py`
+    each never share a cached module; a module whose import raises is not left half-initialised in sys.modules."""
+    import hashlib
     folder = Path(folder).resolve()
+    tag = hashlib.sha1(str(folder).encode()).hexdigest()[:10]
     for path in sorted(folder.rglob('*.py')):
         if '__init__' in path.name:
             continue
-        mod_name = 'mfg_custom_' + '_'.join(path.relative_to(folder).with_suffix('').parts)
+        mod_name = f'mfg_custom_{tag}_' + '_'.join(path.relative_to(folder).with_suffix('').parts)
         mod = sys.modules.get(mod_name)
         if mod is None:
             spec = importlib.util.spec_from_file_location(mod_name, path)
             mod = importlib.util.module_from_spec(spec)
             sys.modules[mod_name] = mod
-            spec.loader.exec_module(mod)
+            try:
+                spec.loader.exec_module(mod)
+            except BaseException:
+                sys.modules.pop(mod_name, None)
+                raise
+        yield mod
+
+
+def locate_custom_class(name, folder):
+    """The class `name` from the first module under `folder` that defines it (helpers.py:215-250)."""
+    for mod in custom_modules(folder):
         if hasattr(mod, name):
             return getattr(mod, name)
     return None
@@ -158,14 +181,70 @@ class GroupView(list):
         return f'{self.name}[{len(self)}]'
 
 
-def _pos_dict(groups):
-    """`entities.pos_dict` (groups/global_entities.py): entities by position, walls and agents first."""
+class PosDict(dict):
+    """`entities.pos_dict` (groups/global_entities.py, a defaultdict(list)): entities by position, walls and
+    agents first. `stale` {cell: message}: the cells whose entries a device rule later in the step changes
+    (pre- and end-of-step positions of a whole-group mutator's entities); reading one raises StaleStateError,
+    and so does walking the whole dict (its key set may differ from the hook's). Every other cell is exact."""
+
+    def __init__(self, items=(), stale=None):
+        super().__init__(items)
+        self._stale = stale or {}
+
+    def _check(self, pos):
+        msg = self._stale.get(tuple(pos)) if isinstance(pos, (tuple, list)) else None
+        if msg:
+            raise StaleStateError(msg)
+
+    def _check_all(self):
+        if self._stale:
+            raise StaleStateError(next(iter(self._stale.values())))
+
+    def __missing__(self, pos):
+        self._check(pos)
+        return []
+
+    def __getitem__(self, pos):
+        self._check(pos)
+        return super().__getitem__(pos)
+
+    def get(self, pos, default=None):
+        self._check(pos)
+        return super().get(pos, default)
+
+    def __contains__(self, pos):
+        self._check(pos)
+        return super().__contains__(pos)
+
+    def __iter__(self):
+        self._check_all()
+        return super().__iter__()
+
+    def keys(self):
+        self._check_all()
+        return super().keys()
+
+    def values(self):
+        self._check_all()
+        return super().values()
+
+    def items(self):
+        self._check_all()
+        return super().items()
+
+    def __len__(self):
+        self._check_all()
+        return super().__len__()
+
+
+def _pos_dict(groups, stale=None):
+    """`entities.pos_dict` of the view's groups (see PosDict)."""
     pos_dict = {}
     for g in ('Walls', 'Agents') + tuple(x for x in groups if x not in ('Walls', 'Agents', 'Batteries')):
         for e in groups[g]:
             if e.pos != NO_POS:
                 pos_dict.setdefault(e.pos, []).append(e)
-    return pos_dict
+    return PosDict(pos_dict, stale)
 
 
 class StateView:
@@ -209,14 +288,18 @@ class StateView:
         self._groups = groups
         self.entities = _Frozen(pos_dict=_pos_dict(groups), names=list(groups), floorlist_cells=len(spec.floor_cells))
 
-    def restricted(self, stale, who):
-        """This view with the reads in `stale` ({group: (attrs | None, device rule)}) refused for rule `who`."""
+    def restricted(self, stale, who, before=None):
+        """This view with the reads in `stale` ({group: (attrs | None, device rule)}) refused for rule `who`.
+        A whole-group entry refuses the group and the pos_dict cells its entities occupy in this view or in
+        `before` (the view before the step: where they stood at the hook); attribute entries refuse those
+        attributes on the group's entities, and on the agents Batteries are bound to."""
         if not stale:
             return self
         v = object.__new__(StateView)
         v.spec, v.snap, v.curr_step = self.spec, self.snap, self.curr_step
         v._whole = {}
         groups = dict(self._groups)
+        cells = {}
         for g, (attrs, dev) in stale.items():
             if g not in groups:
                 continue
@@ -224,12 +307,30 @@ class StateView:
                    f'device rule {dev!r} changes later in the step; the host view only holds the end-of-step state')
             if attrs is None:
                 v._whole[g] = msg
+                if g == 'DirtPiles' and before is not None and 'DirtPiles' in before._groups:
+                    # RespawnDirt only adds piles or tops them up, at free cells (clean_up/groups.py:70-95,
+                    # states.py:144-151); agents' Clean actions only lower amounts: the cells it changed are those
+                    # with a new pile or a higher amount than before the step
+                    was = {e.pos: e.amount for e in before._groups['DirtPiles']}
+                    for e in groups[g]:
+                        if e.pos != NO_POS and (e.pos not in was or e.amount > was[e.pos]):
+                            cells.setdefault(e.pos, msg)
+                elif g != 'Batteries':
+                    for src in (groups[g], before._groups.get(g, ()) if before is not None else ()):
+                        for e in src:
+                            if e.pos != NO_POS:
+                                cells.setdefault(e.pos, msg)
             else:
                 groups[g] = GroupView(g, [type(e)(_stale={a: msg for a in attrs}, **e._d) for e in groups[g]])
+        if 'Batteries' in groups and groups['Agents'] is not self._groups['Agents']:
+            by_name = {a.name: a for a in groups['Agents']}  # bound_entity -> the restricted agent view
+            groups['Batteries'] = GroupView('Batteries', [
+                type(b)(_stale=b._stale, **dict(b._d, bound_entity=by_name.get(b._d['bound_entity'].name,
+                                                                                 b._d['bound_entity'])))
+                for b in groups['Batteries']])
         v._groups = groups
-        pos_msg = next((m for g, m in v._whole.items() if g != 'Batteries'), None)
-        kw = dict(self.entities._d, pos_dict=_pos_dict(groups))
-        v.entities = _Frozen(_stale={'pos_dict': pos_msg} if pos_msg else None, **kw)
+        kw = dict(self.entities._d, pos_dict=_pos_dict(groups, cells))
+        v.entities = _Frozen(**kw)
         return v
 
     def __getitem__(self, key):
@@ -265,8 +366,7 @@ class HostRules:
     def __init__(self, spec):
         self.spec = spec
         self.rules = [(slot, cls(**(kw or {}))) for slot, name, cls, kw in spec.host_rules]
-        self.stale = [{ph: stale_state(spec, slot, ph) for ph in (_info.TICK, _info.POST)}
-                      for slot, _, _, _ in spec.host_rules]
+        self._stale_cache = {}
         self.rule_names = [name for _, name, _, _ in spec.host_rules]
         self.names = [f'Agent[{n}]' for n in spec.agent_names]
 
@@ -282,16 +382,21 @@ class HostRules:
             r.on_reset(view)
             r.on_reset_post_spawn(view)
 
-    def step_results(self, views):
+    def step_results(self, views, fired=None):
         """Host results per phase, tagged with their rule slot (ahead of the device rule at that index).
         views: {phase: StateView} -- PRE: the state before the step (curr_step already advanced, agent states
         cleared, states.py:181-187); TICK: positions after the agents' actions with their action results as
-        agent states; POST / DONE: the end of the step (WatchCollisions' states included)."""
+        agent states; POST / DONE: the end of the step (WatchCollisions' states included).
+        fired: device rule indices that emitted a Result this step (stale_state)."""
         out = []
+        key = None if fired is None else frozenset(fired)
         for phase, hook in ((_info.PRE, 'tick_pre_step'), (_info.TICK, 'tick_step'), (_info.POST, 'tick_post_step'),
                             (_info.DONE, 'on_check_done')):
             for k, (slot, r) in enumerate(self.rules):
-                view = views[phase].restricted(self.stale[k].get(phase), self.rule_names[k])
+                cache = self._stale_cache.setdefault((k, phase), {})
+                if key not in cache:
+                    cache[key] = stale_state(self.spec, slot, phase, fired)
+                view = views[phase].restricted(cache[key], self.rule_names[k], before=views[_info.PRE])
                 for x in getattr(r, hook)(view) or []:
                     out.append(_as_res(x, phase, slot - 0.5, self.names))
         return out
@@ -317,9 +422,11 @@ def fold_step(spec, host, actions, ev, pre, post, device_done):
     states = _views.agent_states(spec, actions, act, [0] * spec.n_agents)
     tick = dataclasses.replace(post, agents=[(c, s, v) for (c, _, _), (s, v) in zip(post.agents, states)])
     fv = StateView(spec, post)
+    dres = _info.step_results(spec, actions, ev)
+    fired = {r.slot for r in dres if r.slot >= 0}
     hres = host.step_results({_info.PRE: StateView(spec, pre), _info.TICK: StateView(spec, tick),
-                              _info.POST: fv, _info.DONE: fv})
-    merged = HostRules.merge(_info.step_results(spec, actions, ev), hres)
+                              _info.POST: fv, _info.DONE: fv}, fired)
+    merged = HostRules.merge(dres, hres)
     reward = _info.rebuild_rewards(spec, merged)
     info = _info.rebuild_info(spec, actions, ev, reward, results=merged)
     done = bool(device_done) or any(r.valid for r in hres if r.phase == _info.DONE)

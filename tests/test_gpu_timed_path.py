@@ -1,9 +1,10 @@
 """GPU parity of the exact mode bench.py times:
-  * mfg_step with K=8 fused steps, Philox actions (actions=None), float32 obs, auto-reset, at the headline
-    batch B=65536 on large8 (C3), for 608 steps (across the 500-step episode boundary). 256 envs spread
-    over the batch (incl. 0 and B-1) are checked every step against their own C-oracle env: f64 rewards
-    with ==, done, the event rows, obs bit-equal to the oracle's f64 obs cast to float32, and after every
-    call (one k_replay each) the MT19937 state and floor order.
+  * mfg_step with K=8 fused steps, Philox actions (actions=None), f64 obs (the headline line since round 4, the
+    reference's own obs precision) and float32 obs (its side line), auto-reset, at the headline batch B=65536 on
+    large8 (C3), for 608 steps (across the 500-step episode boundary). 256 envs spread over the batch (incl. 0
+    and B-1) are checked every step against their own C-oracle env: f64 rewards with ==, done, the event rows,
+    obs bit-equal to the oracle's f64 obs (cast to float32 for the f32 mode), and after every call (one k_replay
+    each) the MT19937 state and floor order.
   * K=8 and K=1 calls give identical outputs and identical state (the cross-call shuffle-debt carry and the
     per-k output offsets), on large8 and on the step-RNG paths (dirt respawn, maintainers).
   * the documented row widths of include/mfg.h: guard words after every output buffer stay untouched.
@@ -46,6 +47,15 @@ def _sha(a):
 
 @pytest.mark.timeout(900)
 def test_timed_path_k8_fp32_b65536_matches_oracle():
+    _timed_path(np.float32)
+
+
+@pytest.mark.timeout(900)
+def test_timed_path_k8_f64_b65536_matches_oracle():
+    _timed_path(np.float64)
+
+
+def _timed_path(odt):
     import oracle as O
     from philox import synthetic_actions
     from mfg_amd.engine import RecordView, events_from_rows
@@ -55,14 +65,15 @@ def test_timed_path_k8_fp32_b65536_matches_oracle():
     rng = np.random.default_rng(3)
     idx = np.unique(np.concatenate([[0, 1, B // 2, B - 2, B - 1], rng.choice(B, 251, replace=False)]))
     idx_t = torch.as_tensor(idx, device=eng.device)
-    buf = _buffers(torch, eng, K, torch.float32)
+    buf = _buffers(torch, eng, K, torch.float32 if odt == np.float32 else torch.float64)
+    ubits = np.uint32 if odt == np.float32 else np.uint64
     eng.reset(obs=buf['obs'][0], init=True, seed_base=base)
     envs = [O.OracleEnv(spec, base + int(i)) for i in idx]
     o0 = buf['obs'][0][idx_t].cpu().numpy()
     for j, env in enumerate(envs):
         ro = env.reset()
         for a in range(A):
-            assert (o0[j, a, :nl[a]] == ro[a].astype(np.float32)).all(), f'reset obs env {idx[j]} agent {a}'
+            assert (o0[j, a, :nl[a]] == ro[a].astype(odt)).all(), f'reset obs env {idx[j]} agent {a}'
     ndone = 0
     step = 0
     for c in range(calls):
@@ -90,11 +101,11 @@ def test_timed_path_k8_fp32_b65536_matches_oracle():
                 else:
                     ro = env.obs_list()
                 for a in range(A):
-                    want = ro[a].astype(np.float32)
+                    want = ro[a].astype(odt)
                     got = ob[k, j, a, :nl[a]]
-                    if not (got.view(np.uint32) == want.view(np.uint32)).all():
+                    if not (got.view(ubits) == want.view(ubits)).all():
                         dif = np.argwhere(got != want)
-                        raise AssertionError(f'{tag} agent {a} fp32 obs: {len(dif)} diffs, first '
+                        raise AssertionError(f'{tag} agent {a} {odt.__name__} obs: {len(dif)} diffs, first '
                                              f'{[(tuple(x), got[tuple(x)], want[tuple(x)]) for x in dif[:4]]}')
         step += K
         # after the call's k_replay: RNG state and floor order of the sampled envs

@@ -185,3 +185,126 @@ def test_stale_reads_refused(tmp_path, compat_path):
     run({**close, 'DoorTimerReader': None})  # after DoorAutoClose: the end-of-step timers are the hook's
     with pytest.raises(StaleStateError, match='DoorAutoClose'):
         run({'DoorTimerReader': None, **close})
+
+
+_POS_READERS = '''
+from marl_factory_grid.environment.rules import Rule
+from marl_factory_grid.utils.results import TickResult
+
+
+class PosDictReader(Rule):
+    """tick_step: the common `pos_dict[agent.pos]` pattern, one value per agent (entities on its cell)."""
+    def tick_step(self, state):
+        return [TickResult(self.name, validity=True, value=len(state.entities.pos_dict[a.pos]), entity=a)
+                for a in state['Agents']]
+
+
+class PosDictWalker(Rule):
+    """tick_step: walks the whole pos_dict (its key set changes when RespawnDirt spawns later in the hook)."""
+    def tick_step(self, state):
+        return [TickResult(self.name, validity=True, value=len(list(state.entities.pos_dict.items())))]
+
+
+class BatteryPostReader(Rule):
+    """tick_post_step: battery charge (BatteryDecharge changes it in tick_step only, batteries/rules.py:50-87)."""
+    def tick_post_step(self, state):
+        return [TickResult(self.name, validity=True, value=sum(b.charge_level for b in state['Batteries']))]
+
+
+class BoundStateReader(Rule):
+    """tick_post_step: an agent's state through its battery (WatchCollisions rewrites agent states later)."""
+    def tick_post_step(self, state):
+        return [] if any(b.bound_entity.state is None for b in state['Batteries']) else []
+'''
+
+
+def _run_custom(tmp_path, cfg_name, rules, steps, actions=None, dirt=None):
+    import oracle as O
+    import yaml
+    from views_compare import oracle_snapshot
+    from mfg_amd.spec import compile_spec
+    from mfg_amd.host_rules import HostRules, fold_step, pre_snapshot
+    (tmp_path / 'mods').mkdir(exist_ok=True)
+    (tmp_path / 'mods' / 'posreaders.py').write_text(_POS_READERS)
+    base = yaml.safe_load((ROOT / 'marl-factory-grid_amd' / 'mfg_amd' / 'configs' / cfg_name).read_text())
+    cfg = dict(base, Rules=rules)
+    if dirt:
+        cfg['Entities']['DirtPiles'].update(dirt)
+    p = tmp_path / 'cfg.yaml'
+    p.write_text(yaml.safe_dump(cfg, sort_keys=False))
+    spec = compile_spec(p, custom_modules_path=str(tmp_path / 'mods'))
+    env = O.OracleEnv(spec, 0)
+    env.reset()
+    host = HostRules(spec)
+    rng = random.Random(7)
+    out = []
+    try:
+        for t in range(steps):
+            acts = actions or [rng.randrange(n) for n in spec.n_actions]
+            pre = pre_snapshot(oracle_snapshot(env))
+            _, ddone, ev = env.step(acts, with_obs=False)
+            out.append(fold_step(spec, host, acts, ev, pre, oracle_snapshot(env), ddone))
+            if ddone:
+                env.reset()
+    finally:
+        env.close()
+    return spec, out
+
+
+def test_pos_dict_reader_under_clean_and_bring(tmp_path, compat_path):
+    """ADVICE r3: `pos_dict[agent.pos]` in a tick_step placed ahead of every device rule of clean_and_bring
+    (smear, doors, RespawnDirt, RespawnItems, WatchCollisions) stays readable on every step, spawn steps
+    included: RespawnItems and smearing never change state (Q9, Q1), and RespawnDirt only adds dirt at free cells
+    (no agent), so only those cells are refused. Walking the whole pos_dict is refused on a spawn step only."""
+    from mfg_amd.host_rules import StaleStateError, stale_state
+    from mfg_amd import info as I
+    rules = {'PosDictReader': None, 'EntitiesSmearDirtOnMove': {'smear_ratio': 0.2},
+             'DoorAutoClose': {'close_frequency': 7}, 'RespawnDirt': {'respawn_freq': 5},
+             'RespawnItems': {'respawn_freq': 50}, 'WatchCollisions': {'done_at_collisions': False},
+             'DoneAtMaxStepsReached': {'max_steps': 500}}
+    spec, out = _run_custom(tmp_path, 'clean_and_bring.yaml', rules, 40, dirt={'max_global_amount': 1000})
+    assert len(out) == 40
+    st = stale_state(spec, 0, I.TICK)
+    assert set(st) == {'Doors', 'DirtPiles'}  # no Items (Q9), no smear (Q1)
+    assert sum('Global_DirtPiles_spawn' in info for _, _, info in out) >= 6  # spawns happened (steps 6, 12, ...)
+    # the same reader walking the whole dict: refused exactly on the RespawnDirt spawn steps
+    walker = dict(rules)
+    walker.pop('PosDictReader')
+    walker = {'PosDictWalker': None, **walker}
+    _run_custom(tmp_path, 'clean_and_bring.yaml', walker, 5, dirt={'max_global_amount': 1000})  # no spawn yet
+    with pytest.raises(StaleStateError, match='RespawnDirt'):
+        _run_custom(tmp_path, 'clean_and_bring.yaml', walker, 8, dirt={'max_global_amount': 1000})
+
+
+def test_battery_reads_after_tick_and_bound_agent_states(tmp_path, compat_path):
+    """ADVICE r3: battery charge is readable in tick_post_step (BatteryDecharge changes it in tick_step only), and
+    an agent state reached through Battery.bound_entity is refused like Agents[i].state when WatchCollisions
+    rewrites agent states later in tick_post_step."""
+    from mfg_amd.host_rules import StaleStateError
+    base = {'BatteryDecharge': {'initial_charge': 0.8, 'per_action_costs': 0.02}, 'DoneAtMaxStepsReached':
+            {'max_steps': 500}}
+    _, out = _run_custom(tmp_path, 'large8.yaml', {'BatteryPostReader': None, **base}, 6)
+    assert all(any(k.endswith('BatteryPostReader') for k in info) for _, _, info in out)
+    with pytest.raises(StaleStateError, match='WatchCollisions'):
+        _run_custom(tmp_path, 'large8.yaml', {'BoundStateReader': None, **base, 'WatchCollisions': None}, 3)
+    _run_custom(tmp_path, 'large8.yaml', {**base, 'WatchCollisions': None, 'BoundStateReader': None}, 3)
+
+
+def test_custom_module_cache_is_per_folder(tmp_path, compat_path):
+    """ADVICE r3: two custom folders that both hold `rules.py` are loaded as different modules (the explainer and
+    the spec compiler's lookup share host_rules.custom_modules), and a module whose import fails leaves no
+    half-initialised entry behind."""
+    from mfg_amd.explain import _custom_rules
+    from mfg_amd.host_rules import locate_custom_class
+    hdr = 'from marl_factory_grid.environment.rules import Rule\n\n\n'
+    for name, cls in (('a', 'RuleA'), ('b', 'RuleB')):
+        (tmp_path / name).mkdir()
+        (tmp_path / name / 'rules.py').write_text(hdr + f'class {cls}(Rule):\n    pass\n')
+    assert list(_custom_rules(tmp_path / 'a')) == ['RuleA']
+    assert list(_custom_rules(tmp_path / 'b')) == ['RuleB']
+    assert locate_custom_class('RuleB', tmp_path / 'b').__name__ == 'RuleB'
+    (tmp_path / 'c').mkdir()
+    (tmp_path / 'c' / 'rules.py').write_text('raise ImportError("broken plugin")\n')
+    for _ in range(2):  # the failed import is retried, not served half-initialised from sys.modules
+        with pytest.raises(ImportError, match='broken plugin'):
+            locate_custom_class('X', tmp_path / 'c')
