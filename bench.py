@@ -369,7 +369,8 @@ def main():
     eng.reset(obs=obs[0], init=True, seed_base=env_base)
     stream = torch.cuda.current_stream(dev)
     step_no = 0
-    episodes = torch.zeros((), dtype=torch.float64, device=dev)
+    red_dev = dev if world == 1 or args.backend == 'nccl' else torch.device('cpu')  # gloo reduces host tensors
+    episodes = torch.zeros((), dtype=torch.float64, device=red_dev)
 
     def run(n, events=None, profile=False, obs_buf=None, after=None):
         """n steps in calls of F (the last call may be shorter). Per-kernel HIP events are recorded only
@@ -412,10 +413,10 @@ def main():
     prof = eng.profile_read()
     eng.profile(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        episodes += done.double().sum()
+        episodes += done.double().sum().to(red_dev)
         dist.all_reduce(episodes)  # optional metrics all-reduce (tiny, latency-bound)
     total = B * world * args.steps
     value = total / elapsed
@@ -434,7 +435,7 @@ def main():
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t1
         if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el

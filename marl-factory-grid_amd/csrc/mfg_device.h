@@ -101,7 +101,7 @@ struct MfgDevSpec {
   const int32_t* floor_init; // [nf]
   const int8_t* ray_pts;     // [nrays][maxpts][2] (dx, dy), padded
   const uint8_t* ray_len;    // [nrays]
-  const uint32_t* ray_diag;  // [nrays] bit p: point p is a diagonal step from point p-1 (ray_caster.py:89-96)
+  const uint64_t* ray_diag;  // [nrays] bit p: point p is a diagonal step from point p-1 (ray_caster.py:89-96)
   // [nf][nrays][3] per ray origin (floor index) and ray: the light-blocking bits of its points that depend
   // only on the static level (bit p: a wall at point p; a diagonal cut between two walls at step p), and
   // the points whose blocking depends on a door (recomputed from the cell map at render time). Null:

@@ -379,8 +379,8 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   {  // points per ray (<= fr + 1), rounded up to a compiled k_obs instantiation (DISPATCH_MP)
     int mp = 1;
     for (int r = 0; r < h.nrays; r++) mp = std::max(mp, s->ray_off[r + 1] - s->ray_off[r]);
-    if (mp > 32) { delete e; return fail("rays longer than 32 points"); }
-    static const int SIZES[] = {4, 6, 8, 10, 12, 14, 16, 18, 24, 32};
+    if (mp > 64) { delete e; return fail("rays longer than 64 points"); }
+    static const int SIZES[] = {4, 6, 8, 10, 12, 14, 16, 18, 24, 32, 48, 64};
     for (int k : SIZES) if (k >= mp) { h.maxpts = k; break; }
   }
   int lmax = 1;
@@ -526,7 +526,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   }
   std::vector<int8_t> rp((size_t)h.nrays * h.maxpts * 2, 0);
   std::vector<uint8_t> rlen(h.nrays);
-  std::vector<uint32_t> rdiag(h.nrays, 0u);
+  std::vector<uint64_t> rdiag(h.nrays, 0ull);
   for (int r = 0; r < h.nrays; r++) {
     const int p0 = s->ray_off[r], p1 = s->ray_off[r + 1];
     if (p1 - p0 > h.maxpts || p1 - p0 > h.fr + 1) { delete e; return fail("ray longer than its radius + 1 points"); }
@@ -536,7 +536,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     rlen[r] = (uint8_t)(p1 - p0);
     for (int p = p0 + 1; p < p1; p++)
       if (s->ray_pts[2 * p] != s->ray_pts[2 * p - 2] && s->ray_pts[2 * p + 1] != s->ray_pts[2 * p - 1])
-        rdiag[r] |= 1u << (p - p0);
+        rdiag[r] |= 1ull << (p - p0);
     for (int p = p0; p < p1; p++) {
       rp[((size_t)r * h.maxpts + (p - p0)) * 2] = (int8_t)s->ray_pts[2 * p];
       rp[((size_t)r * h.maxpts + (p - p0)) * 2 + 1] = (int8_t)s->ray_pts[2 * p + 1];
@@ -552,9 +552,10 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
   rc |= upload(e, rdiag.data(), rdiag.size(), &h.ray_diag);
   {  // static light-blocking table per (origin floor cell, ray): walls only; door-dependent points flagged
+    // (32-bit point masks: rays of up to 32 points; longer rays test every point against the cell map)
     const size_t n = (size_t)s->n_floor * h.nrays * 3;
     h.ray_static = nullptr;
-    if (n * 4 <= ((size_t)256 << 20) && !MFG_NO_RAY_STATIC) {
+    if (n * 4 <= ((size_t)256 << 20) && !MFG_NO_RAY_STATIC && h.maxpts <= 32) {
       std::vector<uint32_t> rs(n, 0u);
       auto wall = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && s->level[x * s->W + y] == 1; };
       auto door = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && door_of[x * s->W + y] != 0xFF; };
@@ -809,6 +810,8 @@ static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipS
     case 18: { constexpr int MP = 18; CALL; } break; \
     case 24: { constexpr int MP = 24; CALL; } break; \
     case 32: { constexpr int MP = 32; CALL; } break; \
+    case 48: { constexpr int MP = 48; CALL; } break; \
+    case 64: { constexpr int MP = 64; CALL; } break; \
     default: return fail("unsupported ray length"); \
   }
 

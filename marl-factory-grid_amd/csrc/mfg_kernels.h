@@ -76,6 +76,7 @@ static_assert(!(MFG_RPV & 1) || (MFG_RPV & 2), "MFG_RPV bit 1 (no read sink) nee
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <type_traits>
 
 #include "mfg_device.h"
 
@@ -2419,13 +2420,17 @@ __device__ void build_cmap(const Env& e, int wv = 0, int nwv = 1) {
   wave_sync();
 }
 
-// One ray per lane: packed (dx, dy) int8 offsets of up to MAXPTS points and the ray length.
+// One ray per lane: packed (dx, dy) int8 offsets of up to MAXPTS points and the ray length. Point masks are 32-bit
+// for rays of up to 32 points, 64-bit above (pomdp_r 16..31, full observability on levels with min(H, W) <= 63).
 template <int MAXPTS>
 struct RayLane {
+  static_assert(MAXPTS <= 64, "rays of at most 64 points");
+  typedef typename std::conditional<(MAXPTS > 32), u64, uint32_t>::type PM;  // one bit per point
+  static constexpr int RSH = MAXPTS > 32 ? 6 : 5;  // first-visit rank = ray << RSH | point
   static constexpr int NW = (2 * MAXPTS + 3) / 4;
   uint32_t pk[NW];  // byte 2p = dx of point p, byte 2p+1 = dy (sign-extended on use)
   int len;
-  uint32_t diag;    // bit p: point p is a diagonal step
+  PM diag;          // bit p: point p is a diagonal step
   __device__ __forceinline__ int dx(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16)) & 0xFF); }
   __device__ __forceinline__ int dy(int p) const { return (int)(int8_t)((pk[p >> 1] >> ((p & 1) * 16 + 8)) & 0xFF); }
   static_assert(MAXPTS % 2 == 0 && NW * 4 == 2 * MAXPTS, "a ray's points are whole dwords");
@@ -2437,7 +2442,7 @@ struct RayLane {
 #pragma unroll
     for (int q = 0; q < NW; q++) pk[q] = pts[q];
     len = has ? S->ray_len[ray] : 0;
-    diag = has ? S->ray_diag[ray] : 0u;
+    diag = has ? (PM)S->ray_diag[ray] : (PM)0;
   }
 };
 
@@ -2624,7 +2629,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     npairs = uni(e.hdrp[MFG_HDR_N - 1]);
   }
   // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
-  // ray * 32 + point; it gives both the window visibility and the dedupe order (Q14)
+  // ray << 5 | point (ray << 6 | point for rays longer than 32 points); it gives both the window visibility and the
+  // dedupe order (Q14)
   uint32_t* fv = (uint32_t*)(e.scratch + 3 * S->pairs_lds + (MW ? wv * (S->lds_obs_wave >> 2) : 0));
   const int fw = 2 * fr + 1;
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
@@ -2709,8 +2715,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // branch-free: every point tests its cell and (from p = 1) both corner cells; the static diagonal
       // mask keeps the corner test only on diagonal steps: cut when both orthogonal neighbours block
       // light (ray_caster.py:89-96)
-      uint32_t blkm = 0, cutm = 0;
-      if (ofl >= 0) {
+      typedef typename RayLane<MAXPTS>::PM PM;
+      constexpr int NB = 8 * (int)sizeof(PM);
+      PM blkm = 0, cutm = 0;
+      if (MAXPTS <= 32 && ofl >= 0) {  // (no static table for rays longer than 32 points: ofl is -1 there)
         // the wall part from the per-origin table; only points next to doors are tested here (the door's
         // present/closed state lives in the cell map)
         uint32_t dyn;
@@ -2731,38 +2739,38 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
           dyn &= dyn - 1;
           const int8_t* pt = S->ray_pts + ((size_t)ray_id * S->maxpts + p) * 2;
           const int x = ox + pt[0], y = oy + pt[1];
-          blkm |= light_block_bf<MM>(e, x, y) ? (1u << p) : 0u;
+          blkm |= light_block_bf<MM>(e, x, y) ? ((PM)1 << p) : (PM)0;
           if (p > 0 && ((ray.diag >> p) & 1u)) {
             const bool c = light_block_bf<MM>(e, x, oy + pt[-1]) & light_block_bf<MM>(e, ox + pt[-2], y);
-            cutm |= c ? (1u << p) : 0u;
+            cutm |= c ? ((PM)1 << p) : (PM)0;
           }
         }
       } else {
 #pragma unroll
         for (int p = 0; p < MAXPTS; p++) {
           const int x = ox + ray.dx(p), y = oy + ray.dy(p);
-          blkm |= light_block_bf<MM>(e, x, y) ? (1u << p) : 0u;
+          blkm |= light_block_bf<MM>(e, x, y) ? ((PM)1 << p) : (PM)0;
           if (p > 0) {
             const bool c = light_block_bf<MM>(e, x, oy + ray.dy(p - 1)) & light_block_bf<MM>(e, ox + ray.dx(p - 1), y);
-            cutm |= c ? (1u << p) : 0u;
+            cutm |= c ? ((PM)1 << p) : (PM)0;
           }
         }
       }
       cutm &= ray.diag;
       // points walked: up to and including the first blocking/cut point, within the ray length
-      const uint32_t lenm = ray.len >= 32 ? 0xFFFFFFFFu : ((1u << ray.len) - 1u);
-      const uint32_t stopm = (blkm | cutm) & lenm;
-      const uint32_t walked = stopm ? (((stopm & (0u - stopm)) << 1) - 1u) & lenm : lenm;
+      const PM lenm = ray.len >= NB ? ~(PM)0 : (((PM)1 << ray.len) - (PM)1);
+      const PM stopm = (blkm | cutm) & lenm;
+      const PM walked = stopm ? (((stopm & ((PM)0 - stopm)) << 1) - (PM)1) & lenm : lenm;
       // points outside the grid are recorded too: nothing is there (no entity, no wall), so their
       // first-visit entries are never read (placement tests the grid bounds, pairs are in-grid cells)
-      const uint32_t vism = walked & ~cutm;
+      const PM vism = walked & ~cutm;
       uint32_t* sink = (uint32_t*)(wsup + ((dd + 15) & ~15)) + lane;
       // point 0 of every ray is the origin (checked at mfg_create) and always visible: its entry is
       // ray 0's rank 0, stored once below instead of a 64-lane same-address atomic
 #pragma unroll
       for (int p = 1; p < MAXPTS; p++)
         atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + fr) * fw + ray.dy(p) + fr] : sink,
-                  (uint32_t)(ray_id * 32 + p));
+                  (uint32_t)((ray_id << RayLane<MAXPTS>::RSH) + p));
     }
     if (lane == 0) fv[fr * fw + fr] = 0u;
     wave_sync();

@@ -270,11 +270,12 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None, custom_mo
     pomdp_r = int(gen['pomdp_r'])
     if pomdp_r < 0:
         raise UnsupportedSpec('pomdp_r must be >= 0')
-    # the ray radius is the window diameter (Q13) and a ray's points live in 32-bit masks on the device
-    if pomdp_r > 15:
-        raise UnsupportedSpec('pomdp_r is limited to 15 (rays of <= 32 points)')
-    if pomdp_r == 0 and min(H, W) > 31:
-        raise UnsupportedSpec('full observability (pomdp_r 0) is limited to levels with min(H, W) <= 31')
+    # the ray radius is the window diameter (Q13), so a ray has 2 * pomdp_r + 2 points (min(H, W) + 1 with full
+    # observability); the device keeps a ray's points in one 64-bit mask
+    if pomdp_r > 31:
+        raise UnsupportedSpec('pomdp_r is limited to 31 (rays of <= 64 points)')
+    if pomdp_r == 0 and min(H, W) > 63:
+        raise UnsupportedSpec('full observability (pomdp_r 0) is limited to levels with min(H, W) <= 63')
     d = 2 * pomdp_r + 1
     size = pomdp_r ** 2 if pomdp_r else H * W  # LevelParser.size (level_parser.py:44), collection cap (Q16)
 
