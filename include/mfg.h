@@ -269,6 +269,16 @@ int mfg_abi_version(void);
  * count is validated (returns < 0 instead of reading out of bounds). The caller's current HIP device is
  * restored before any entry point returns; the engine's calls always run on `device`. */
 int mfg_create(const mfg_spec* spec, int device, int64_t n_envs, mfg_engine** out);
+/* Test-only: mfg_create with exact alternative code paths forced, so the parity tests can pin paths the
+ * shipped configs never select (every field 0 = mfg_create's own choice). Results are identical either way. */
+typedef struct mfg_variant {
+  int32_t shuffle_table_path; /* 1: the shuffle blocks' table path (as if the exchange-order probe failed) */
+  int32_t full_temper;        /* 1: the replay's full MT temper (levels with >= 16384 floor cells) */
+  int32_t bfs_hbm;            /* 1: the maintainer BFS scratch in the per-env HBM pool (the grid128 layout) */
+  int32_t pairs_lds;          /* > 0: at most this many identifier pairs in LDS, the rest in the HBM spill */
+} mfg_variant;
+int mfg_create_variant(const mfg_spec* spec, int device, int64_t n_envs, const mfg_variant* variant,
+                       mfg_engine** out);
 int mfg_destroy(mfg_engine* e);
 /* Message of the last failed call on engine e (per engine); e == NULL: the calling thread's last failed
  * mfg_create / argument check. Valid until the next call on the same engine (or thread). */

@@ -2,12 +2,6 @@
 // include/mfg.h, launch shapes, spec upload). Device code: mfg_kernels.h; the observation-render instantiations:
 // mfg_obs_*.hip.
 #include "mfg_kernels.h"
-#ifndef MFG_REPLAY_WPB
-#define MFG_REPLAY_WPB 1  // waves per workgroup of k_replay (compile-time measurement switch)
-#endif
-#ifndef MFG_REPLAY_LPT
-#define MFG_REPLAY_LPT 1  // k_replay envs in longest-debt-first order (0: blockIdx order)
-#endif
 
 // ================================================================================================
 // host side: C-ABI (include/mfg.h)
@@ -28,7 +22,7 @@ struct mfg_engine {
   int rd_slot = 0;     // done list k_logic appends to (alternates per step)
   int rd_blocks = 1;   // k_resetdone workgroups (occupancy x CUs)
   int rpd_blocks = 1;  // k_replay_done workgroups (one wave each)
-  int* rp_hist = nullptr;  // replay order by debt (MFG_REPLAY_LPT): RP_NB bucket counts / offsets
+  int* rp_hist = nullptr;  // replay order by debt : RP_NB bucket counts / offsets
   int* rp_order = nullptr;  // [B] envs in launch order
   uint8_t* rp_key = nullptr;  // [B] bucket per env
   hipStream_t aux = nullptr;  // second stream: resets of a step's done envs and their render (MFG_RESET_OVERLAP)
@@ -252,7 +246,6 @@ __global__ void __launch_bounds__(64) k_probe_xchg(int* bad) {
 }
 
 static int probe_xchg_order(int device) {
-  if (const char* f = getenv("MFG_SHUFFLE_TABLE_PATH")) if (f[0] == '1') return 0;
   (void)device;
   int* d = nullptr;
   int h = -1;
@@ -330,16 +323,21 @@ static int validate_spec(const mfg_spec* s) {
   return 0;
 }
 
-static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out);
-extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out) {
+static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_variant& v, mfg_engine** out);
+extern "C" int mfg_create_variant(const mfg_spec* s, int device, int64_t n_envs, const mfg_variant* v,
+                                  mfg_engine** out) {
   if (!s || !out) return fail("null argument");
   if (n_envs < 1) return fail("n_envs must be >= 1");
   if (validate_spec(s)) return -1;
+  const mfg_variant none{0, 0, 0, 0};
   DevGuard g(device);
-  return create_impl(s, device, n_envs, out);
+  return create_impl(s, device, n_envs, v ? *v : none, out);
+}
+extern "C" int mfg_create(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out) {
+  return mfg_create_variant(s, device, n_envs, nullptr, out);
 }
 
-static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine** out) {
+static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_variant& v, mfg_engine** out) {
   auto* e = new mfg_engine();
   e->device = device;
   e->B = n_envs;
@@ -454,8 +452,8 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   h.bfs_bytes = moving ? align_up(10 * h.nf + 4 * h.nf + 64, 16) : 0;
   h.bfs_off = 0;
   h.bfs_pool = nullptr;
-  const char* force_hbm = getenv("MFG_BFS_HBM");  // test hook: the HBM pool path on small levels too
-  const bool bfs_lds = moving && h.lds_full + h.bfs_bytes <= MFG_LDS_MAX && !(force_hbm && force_hbm[0] == '1');
+  // (mfg_variant.bfs_hbm: the HBM pool path on small levels too, for the parity tests)
+  const bool bfs_lds = moving && h.lds_full + h.bfs_bytes <= MFG_LDS_MAX && !v.bfs_hbm;
   if (bfs_lds) {
     h.bfs_off = h.lds_full;
     h.lds_full = align_up(h.lds_full + h.bfs_bytes, 16);
@@ -476,14 +474,13 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
               8 * MFG_WAVE;  // + packed-mode projection queue
   // replay kernel slice: [hdr 32 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
-    h.xchg_ordered = probe_xchg_order(device);
+    h.xchg_ordered = v.shuffle_table_path ? 0 : probe_xchg_order(device);
     h.replay_mtperm = align_up(4 * 624 + 2 * h.nf, 16);  // o_perm == o_mt + 2496 (make_layout)
     h.replay_sink_off = 4 * RP_HDR_N + h.replay_mtperm;
     h.replay_stab_off = h.replay_sink_off + 2 * MFG_WAVE;  // u16 sinks (replay_shuffle, mt_twist)
     h.replay_stab_n = h.xchg_ordered ? RP_STAB_N : MFG_STAB_N;
     h.lds_replay_per_wave = align_up(h.replay_stab_off + 4 * h.replay_stab_n, 16);
-    const char* ft = getenv("MFG_REPLAY_FULL_TEMPER");  // tests: force the full-temper path
-    h.replay_top14 = h.nf < 16384 && !(ft && ft[0] == '1');
+    h.replay_top14 = h.nf < 16384 && !v.full_temper;  // (mfg_variant.full_temper: that path on small levels)
   }
   pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
   // static tables
@@ -517,7 +514,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
   h.max_pairs += h.n_wd_pairs;
   // LDS holds up to MFG_PAIRS_LDS pairs (the usual case); the bound's remainder spills to an HBM pool
   h.pairs_lds = std::min(h.max_pairs, MFG_PAIRS_LDS);
-  if (const char* f = getenv("MFG_PAIRS_LDS")) h.pairs_lds = std::max(1, std::min(h.pairs_lds, atoi(f)));  // test hook
+  if (v.pairs_lds > 0) h.pairs_lds = std::max(1, std::min(h.pairs_lds, (int)v.pairs_lds));  // mfg_variant
   h.lds_obs += 12 * h.pairs_lds;
   h.lds_obs_shared = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) + 12 * h.pairs_lds;
   h.lds_obs_wave = align_up(h.lds_obs - h.lds_obs_shared, 16);
@@ -555,7 +552,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     // (32-bit point masks: rays of up to 32 points; longer rays test every point against the cell map)
     const size_t n = (size_t)s->n_floor * h.nrays * 3;
     h.ray_static = nullptr;
-    if (n * 4 <= ((size_t)256 << 20) && !MFG_NO_RAY_STATIC && h.maxpts <= 32) {
+    if (n * 4 <= ((size_t)256 << 20) && h.maxpts <= 32) {
       std::vector<uint32_t> rs(n, 0u);
       auto wall = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && s->level[x * s->W + y] == 1; };
       auto door = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && door_of[x * s->W + y] != 0xFF; };
@@ -624,7 +621,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     e->d_bufs.push_back(pool);
     h.pair_pool = (int*)pool;
   }
-  {  // replay launch order (MFG_REPLAY_LPT): debt histogram, per-env bucket, env order
+  {  // replay launch order (longest debt first): debt histogram, per-env bucket, env order
     void* p = nullptr;
     const size_t bytes = 4 * (size_t)RP_NB + (size_t)n_envs + 4 * ((size_t)n_envs + 4);
     if (hipMalloc(&p, bytes) != hipSuccess) {
@@ -694,11 +691,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, mfg_engine
     e->overlap = MFG_RESET_OVERLAP == 2 || (MFG_RESET_OVERLAP == 1 && (long long)h.A * h.nf >= 16384);
     // with long resets (overlap) and a rule that consumes the floor order inside a step, the envs that finish
     // or respawn dirt would otherwise pay up to K steps of debt on the critical path (C4: 6.7 -> 7.4M env-steps/s)
-#ifdef MFG_REPLAY_EACH_STEP
-    e->replay_each = true;
-#else
     e->replay_each = e->overlap && h.step_rng;
-#endif
     // render shape: one wave per env, or (ray length >= 10) one env per workgroup of nwv waves sharing the cell
     // map, whichever keeps more waves per CU (C5: 3 single-wave slices of 49 KB fit a CU, 2 workgroups of 4)
     {
@@ -761,16 +754,9 @@ static int wpb_for(size_t lds) { return (int)std::max<size_t>(1, std::min<size_t
 static unsigned env_grid(const mfg_engine* e, int wpb) { return (unsigned)((e->B + wpb - 1) / wpb); }
 // launch geometry of a kernel with `lds` bytes of dynamic LDS per wave
 #define GEOM(lds) dim3(env_grid(e, wpb_for(lds))), dim3(wpb_for(lds) * 64), (size_t)(lds) * wpb_for(lds)
-// waves per workgroup of k_logic / k_obs (compile-time measurement switches MFG_LOGIC_WPB, MFG_OBS_WPB). k_logic runs
-// one wave per workgroup (C3: 0.1544 -> 0.1507 ms; its slot frees as soon as its env is done); k_obs keeps 4
-// (1 and 2 measured within noise in round 2)
-#ifndef MFG_OBS_WPB
-#define MFG_OBS_WPB MFG_WPB
-#endif
-#ifndef MFG_LOGIC_WPB
-#define MFG_LOGIC_WPB 1
-#endif
-static const int obs_wpb = std::max(1, MFG_OBS_WPB), logic_wpb = std::max(1, MFG_LOGIC_WPB);
+// waves per workgroup of k_logic / k_obs. k_logic runs one wave per workgroup (C3: 0.1544 -> 0.1507 ms; its slot
+// frees as soon as its env is done); k_obs keeps 4 (1 and 2 measured within noise in round 2)
+static const int obs_wpb = MFG_WPB, logic_wpb = 1;
 #define GEOMW(lds, W) dim3(env_grid(e, std::min(W, wpb_for(lds)))), dim3(std::min(W, wpb_for(lds)) * 64), \
     (size_t)(lds) * std::min(W, wpb_for(lds))
 
@@ -892,12 +878,10 @@ static int replay_impl(mfg_engine* e, void* stream) {
   PROF_BEGIN(e, st);
   // one wave per workgroup: a workgroup's slot is held until its slowest env's debt is paid and debts differ
   // per env, so single-wave workgroups free each slot as soon as its env is done (C3: 11.17 -> 10.91 ms per
-  // K=8 launch against 4 waves per workgroup; -DMFG_REPLAY_WPB=W builds the comparison)
-  const int wpb = std::max(1, std::min(MFG_REPLAY_WPB, wpb_for(e->h.lds_replay_per_wave)));
-  // longest debt first (C3: 10.95 -> 10.47 ms per K=8 launch, the order kernels included); -DMFG_REPLAY_LPT=0 off
-  constexpr int lpt = MFG_REPLAY_LPT;
+  // K=8 launch against 4 waves per workgroup)
+  // longest debt first (C3: 10.95 -> 10.47 ms per K=8 launch, the order kernels included)
   const unsigned g256 = (unsigned)((e->B + 255) / 256);
-  if (lpt) {
+  {
     HIPCHK(hipMemsetAsync(e->rp_hist, 0, 4 * RP_NB, st));
     hipLaunchKernelGGL(k_rp_count, dim3(g256), dim3(256), 0, st, e->d_spec, e->d_state, (long long)e->B, e->rp_hist,
                        e->rp_key);
@@ -908,11 +892,10 @@ static int replay_impl(mfg_engine* e, void* stream) {
   if (e->replay2)  // large floor lists: a producer and a consumer wave per env (replay_env2)
     hipLaunchKernelGGL(k_replay2, dim3((unsigned)e->B), dim3(2 * MFG_WAVE),
                        (size_t)e->h.lds_replay_per_wave + RP2_RING, st, e->d_spec, e->d_state, (long long)e->B,
-                       lpt ? (const int*)e->rp_order : nullptr);
+                       (const int*)e->rp_order);
   else
-    hipLaunchKernelGGL(k_replay, dim3((unsigned)((e->B + wpb - 1) / wpb)), dim3(wpb * 64),
-                       (size_t)e->h.lds_replay_per_wave * wpb, st, e->d_spec, e->d_state,
-                       (long long)e->B, lpt ? (const int*)e->rp_order : nullptr);
+    hipLaunchKernelGGL(k_replay, dim3((unsigned)e->B), dim3(64), (size_t)e->h.lds_replay_per_wave, st, e->d_spec,
+                       e->d_state, (long long)e->B, (const int*)e->rp_order);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
   PROF_END(e, st, MFG_K_REPLAY);
@@ -993,11 +976,6 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     // caller's stream renders every other env (k_logic's rd_flag tells k_obs which to leave out): a step's
     // resets are a few hundred latency-bound waves (C4: ~2.4 ms) that the full render hides.
     const bool split = e->overlap && auto_reset && obs_k;
-    // The call's replay (the shuffle debt of all K steps) after the last step's resets, on the second stream
-    // beside the last render: it touches the MT state, the permutation and two header words the render never
-    // reads, and the render's record copy is read-only (its one store, H_OVERFLOW, is another word). The
-    // render then fills the replay's drain (its longest-debt tail) instead of queueing behind it.
-    const bool replay_side = MFG_REPLAY_SIDE && k == K - 1 && obs_k;
     hipStream_t rs = split ? e->aux : st;
     if (split) {
       HIPCHK(hipEventRecord(e->ev_fork, st));
@@ -1019,21 +997,16 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     if (split) {
       const int32_t* lst = e->h.rd_list + (size_t)rd_cur * (size_t)(e->B + 2);
       if (launch_obs(e, obs_k, obs_dtype, rs, k, nullptr, lst, MFG_K_OBS_DONE)) return -1;
-    } else if (replay_side) {  // the resets ran on the caller's stream: fork after them
-      HIPCHK(hipEventRecord(e->ev_fork, st));
-      HIPCHK(hipStreamWaitEvent(e->aux, e->ev_fork, 0));
     }
-    if (replay_side && replay_impl(e, e->aux)) return -1;
     if (split) {
       if (launch_obs(e, obs_k, obs_dtype, st, k, e->h.rd_flag, nullptr, MFG_K_OBS)) return -1;
     } else if (obs_k && launch_obs(e, obs_k, obs_dtype, st, k)) {
       return -1;
     }
-    if (split || replay_side) {
+    if (split) {
       HIPCHK(hipEventRecord(e->ev_join, e->aux));
       HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
     }
-    if (replay_side) return 0;
   }
   return replay_impl(e, stream);
 }

@@ -14,59 +14,17 @@
 //
 // See mfg_device.h for the execution model (one wavefront per env).
 #include <hip/hip_runtime.h>
-#ifndef MFG_OBS_NT
-#define MFG_OBS_NT 1  // k_obs writes the observations with non-temporal stores
-#endif
-// Measurement switches are compile-time only (-D...), never read from the environment at run time:
-//   MFG_NO_RAY_STATIC=1    k_obs tests every ray point against the cell map (no static light table); exact
-//   MFG_REPLAY_EACH_STEP   pay the shuffle debt after every step (default: only for specs with long resets and an
-//                          in-step floor-order consumer); exact
-//   MFG_ABLATE_*           timing-only ablations, results NOT exact (tools/build_ablation.sh)
-//   (other MFG_* switches below select between exact variants for A/B timing)
-#ifndef MFG_NO_RAY_STATIC
-#define MFG_NO_RAY_STATIC 0
-#endif
+// Build switches are compile-time only (-D...); nothing is read from the environment at run time (the parity
+// tests force exact alternative paths through the test-only mfg_create_variant, include/mfg.h):
+//   MFG_RESET_OVERLAP      resets + their renders on a second stream beside the render (below)
+//   MFG_REPLAY2            the two-wave replay: 1 by occupancy (default), 2 always (the parity suite runs it on C2-C4)
+//   MFG_ABLATE_*           timing-only ablations, results NOT exact (tools/build_ablation.sh,
+//                          profiles/r04_replay_ablation.json)
 #ifndef MFG_RESET_OVERLAP
 // mfg_step with auto-reset: the resets + their renders on a second stream beside the other envs' render.
 // 0 never, 1 when the reset is long (agents x floor cells >= 16384: the per-agent floor shuffles and draws of
 // SpawnAgents, C4/C5), 2 always
 #define MFG_RESET_OVERLAP 1
-#endif
-#ifndef MFG_REPLAY_SIDE
-// mfg_step: the call's replay on the second stream beside the last step's render. Measured neutral (C3 34.42/34.70
-// vs 34.72/34.57M env-steps/s, C4 8.94 vs 8.92M) and it blurs the per-kernel times, so it is off by default.
-#define MFG_REPLAY_SIDE 0
-#endif
-#ifndef MFG_RESET_DRAWS
-#define MFG_RESET_DRAWS 1  // SpawnAgents' shuffle(empty_positions) draws on replay_shuffle_t (0: mt_randbelow_seq)
-#endif
-#ifndef MFG_PK_WPE
-#define MFG_PK_WPE 7  // waves per SIMD asked of the short-ray packed render (1: no request)
-#endif
-#ifndef MFG_RESET_INLINE
-#define MFG_RESET_INLINE 1  // env_reset inlined into the reset kernels; k_resetdone asks 4 waves per SIMD (<= 128 VGPRs)
-#endif
-#ifndef MFG_RPD_QUEUE
-#define MFG_RPD_QUEUE 1  // k_replay_done takes done envs from a work queue (0: fixed stride over the list)
-#endif
-#ifndef MFG_PK1_HOIST
-#define MFG_PK1_HOIST 0  // packed entries without the projection: load the first ray pass once per render (1) or per
-                         // agent (0; measured 33.86 vs 33.66M env-steps/s)
-#endif
-#ifndef MFG_OBS_CLAMP
-#define MFG_OBS_CLAMP 1  // k_obs dense placement: lanes past the window duplicate the last cell (no store masks)
-#endif
-#ifndef MFG_RPV
-#define MFG_RPV 3  // k_replay swap-block variant bits (exact; see replay_shuffle_t)
-#endif
-static_assert(!(MFG_RPV & 1) || (MFG_RPV & 2), "MFG_RPV bit 1 (no read sink) needs bit 2 (masked i write)");
-#ifndef MFG_TWIST
-#define MFG_TWIST 1  // MT19937 twist: phases 2/3 take mt[i - 227] from the previous phase's registers (exact)
-#endif
-#ifndef MFG_RPS
-#define MFG_RPS 92  // k_replay chunk arithmetic (exact; 0 = the round-2 form): bit 4 the i-cell address from i,
-                    // bit 8 the exchange's half shift from j, bit 16 the Jacobi seed at 3l/4, bit 64 the consumed
-                    // count on the SALU
 #endif
 #include <stdint.h>
 #include <stdio.h>
@@ -200,7 +158,6 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
 // 454<=i<623: mt[i-227] new). Each phase issues all its LDS reads before any of its writes, so one
 // wave pays three LDS round trips per 624 draws. (Taking mt[i+1] from the neighbour lane by DPP wave_shl
 // instead of a third LDS read was bit-exact and measured no faster: k_replay 11.05-11.12 vs 10.97-11.03 ms.)
-#if MFG_TWIST
 // The third operand of phases 2 and 3, mt[i - 227], is the previous phase's result in the same lane and slot
 // (i - 227 = i0 - 227 + t * 64 + lane), and new[623] takes old[623], new[0] and new[396] from lanes too. So no read
 // waits on a write: the 26 reads of old words are issued first, then the writes, one sync per twist (was 33
@@ -250,52 +207,6 @@ __device__ void mt_twist(const Env& e) {
   if (lane == 0) p[623] = last;
   wave_sync();
 }
-#else
-__device__ void mt_twist(const Env& e) {
-  uint32_t* mt = e.mt();
-  const int lane = e.lane;
-  // lanes outside a phase store into a scratch word instead of branching (no exec-mask juggling);
-  // every kernel that owns MT state has >= 128 B of scratch (two lanes share a sink word)
-  uint32_t* sink = (uint32_t*)e.scratch + (lane >> 1);
-  uint32_t v[4];
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const int i = min(t * MFG_WAVE + lane, 226);
-    v[t] = mt_mix(mt[i], mt[i + 1], mt[i + 397]);
-  }
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const int i = t * MFG_WAVE + lane;
-    *(i < 227 ? &mt[i] : sink) = v[t];
-  }
-  wave_sync();
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const int i = min(227 + t * MFG_WAVE + lane, 453);
-    v[t] = mt_mix(mt[i], mt[i + 1], mt[i - 227]);
-  }
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const int i = 227 + t * MFG_WAVE + lane;
-    *(i < 454 ? &mt[i] : sink) = v[t];
-  }
-  wave_sync();
-#pragma unroll
-  for (int t = 0; t < 3; t++) {
-    const int i = min(454 + t * MFG_WAVE + lane, 622);
-    v[t] = mt_mix(mt[i], mt[i + 1], mt[i - 227]);
-  }
-#pragma unroll
-  for (int t = 0; t < 3; t++) {
-    const int i = 454 + t * MFG_WAVE + lane;
-    *(i < 623 ? &mt[i] : sink) = v[t];
-  }
-  wave_sync();
-  const uint32_t last = mt_mix(mt[623], mt[0], mt[396]);
-  *(lane == 0 ? &mt[623] : sink) = last;
-  wave_sync();
-}
-#endif
 
 // Draw random.randbelow(i+1) for i = hi, hi-1, ..., lo (the inner loop of random.shuffle,
 // random.py:380-395 with _randbelow_with_getrandbits, random.py:239-249). 64 draws are tempered in
@@ -556,26 +467,19 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
     uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
-    // A_l = #accepted lanes < l: Jacobi iteration from the lanes that accept whatever precedes them
-    // (A_l <= l, so c_l >= l accepts for sure)
-#if MFG_RPS & 16  // seed at A_l ~ 3l/4 (the mean acceptance): 1.91 Jacobi rounds per chunk instead of 2.15 (simulated
-                  // over C3's chunks); any seed converges to the same unique fixed point (lane l is exact after l rounds)
+    // A_l = #accepted lanes < l: Jacobi iteration from a seed at A_l ~ 3l/4 (the mean acceptance; 1.91 rounds per
+    // chunk instead of 2.15 from the sure lower bound c_l >= l, simulated over C3's chunks). Any seed converges to
+    // the same unique fixed point (lane l is exact after l rounds).
     u64 m = ballot(c >= lane34);
-#else
-    u64 m = ballot(c >= lane);
-#endif
 #ifdef MFG_ABLATE_NOJACOBI  // timing only: the seed taken as the accepted set (no fixed-point iteration)
     const int A = mbcnt(m);
 #else
     const int A = accept_ranks(m, c);
 #endif
     const int nacc = popc(m);
-#if MFG_RPS & 64  // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1),
-                  // and then exactly the lanes up to the last accepted one (scalar, no vector compare)
+    // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1), and then
+    // exactly the lanes up to the last accepted one (scalar, no vector compare)
     const int consumed = nacc > span ? 64 - __builtin_clzll(m) : 64;
-#else
-    const int consumed = popc(ballot(A <= span));
-#endif
     const int inext = icur - nacc, idxn = idx + consumed;
 #ifndef MFG_ABLATE_NOSWAP
     if constexpr (!SWAP) {
@@ -585,12 +489,9 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // (a chunk with no accepted draw runs the block on the sinks: rare, and one branch less per chunk)
     const bool acc = lanes(m);
     const int i = icur - A, j = (int)r;
-    uint16_t* const ptop = perm + icur;  // wave-uniform
-#if MFG_RPV & 1  // rejected lanes read the next accepted rank's cell (same address: a broadcast, no sink bank)
-    uint16_t* pi = (MFG_RPS & 4) ? perm + i : ptop - A;  // RPS 4: the address on the VALU
-#else
-    uint16_t* pi = acc ? ptop - A : sink;
-#endif
+    // every lane reads its i cell: rejected lanes read the next accepted rank's cell (the same address as that
+    // lane: a broadcast, no sink bank); only accepted lanes write it back
+    uint16_t* pi = perm + i;
     int v = (int)*pi;
     // V_t (value leaving i_t): if earlier draws s < t moved a value onto i_t (j_s == i_t, i.e. j_s in
     // the block's own i range (inext, i)), the last one's V_s. Rare at large i: a single scalar test
@@ -601,12 +502,6 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     u64 cm = ballot(j > inext) & ballot(j < i) & m;
 #ifdef MFG_ABLATE_NOFWD
     cm = 0;
-#endif
-#ifdef MFG_ABLATE_NOFWD_SERIAL
-    if (popc(cm) <= RP_SERIAL_FWD) cm = 0;
-#endif
-#ifdef MFG_ABLATE_NOFWD_TABLE
-    if (popc(cm) > RP_SERIAL_FWD) cm = 0;
 #endif
     if (cm) {
       if (popc(cm) <= RP_SERIAL_FWD) {
@@ -633,27 +528,10 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
         }
       }
     }
-    // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j].
-    // The next chunk's MT words are loaded while the exchange is in flight.
-#if MFG_RPV & 4  // rejected lanes: a no-op (mask 0) on their own rank-table dword instead of a shared u16 sink
-    uint32_t F;
-    {
-      const uint32_t ja = (uint32_t)(uintptr_t)&perm[j];
-      const uint32_t sh = (ja & 2u) << 3;
-      const uint32_t ad = acc ? (ja & ~3u) : (uint32_t)(uintptr_t)&ptab[lane];
-      const uint32_t mk = acc ? 0xFFFFu << sh : 0u, dt = acc ? (uint32_t)v << sh : 0u;
-      asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(F) : "v"(ad), "v"(mk), "v"(dt) : "memory");
-      if (idxn <= 560) yw = mt[idxn + lane];
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F) : : "memory");
-      F = (F >> sh) & 0xFFFFu;
-    }
-#elif MFG_RPV & 8  // rejected lanes exec-masked out of the exchange
-    uint32_t F = 0;
-    if (acc) F = lds_xchg_u16_issue(&perm[j], (uint32_t)v);
-    if (idxn <= 560) yw = mt[idxn + lane];
-    F = lds_xchg_u16_wait(F, &perm[j]);
-#elif MFG_RPS & 8  // the half's shift from j: shifts read the low 5 bits, so j << 4 is (j & 1) * 16 (perm is
-                   // dword aligned in every LDS image); rejected lanes edit either half of their sink word
+    // F = value landing on i: the exchange returns the previous same-address draw's V or P0[j]. The 16-bit half's
+    // shift comes from j: shifts read the low 5 bits, so j << 4 is (j & 1) * 16 (perm is dword aligned in every LDS
+    // image); rejected lanes edit either half of their sink word. The next chunk's MT words are loaded while the
+    // exchange is in flight.
     uint32_t F;
     {
       const uint32_t sh = (uint32_t)j << 4;
@@ -664,16 +542,7 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F) : : "memory");
       asm("v_lshrrev_b32 %0, %1, %2" : "=v"(F) : "v"(sh), "v"(F));  // low 5 bits of sh; the i write keeps 16 bits
     }
-#else
-    uint32_t F = lds_xchg_u16_issue(acc ? &perm[j] : sink, (uint32_t)v);
-    if (idxn <= 560) yw = mt[idxn + lane];
-    F = lds_xchg_u16_wait(F, acc ? &perm[j] : sink);
-#endif
-#if MFG_RPV & 2  // only accepted lanes write their i cell (exec mask) instead of rejected lanes writing a sink
     if (acc) *pi = (uint16_t)F;
-#else
-    *pi = (uint16_t)F;
-#endif
     wave_sync();
     }
 #else
@@ -735,17 +604,10 @@ __device__ void rp2_produce(const Env& e, uint8_t* half, int* cnt, Rp2Prod& st, 
     const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);
     const uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
-#if MFG_RPS & 16  // the single-wave replay's seed and consumed count (replay_shuffle_t)
-    u64 m = ballot(c >= (3 * lane) >> 2);
+    u64 m = ballot(c >= (3 * lane) >> 2);  // the single-wave replay's seed and consumed count (replay_shuffle_t)
     const int A = accept_ranks(m, c);
     const int nacc = popc(m);
     const int consumed = nacc > span ? 64 - __builtin_clzll(m) : 64;
-#else
-    u64 m = ballot(c >= lane);
-    const int A = accept_ranks(m, c);
-    const int consumed = popc(ballot(A <= span));
-    const int nacc = popc(m);
-#endif
     uint8_t* rec = half + n * RP2_REC;
     if (lanes(m)) ((uint16_t*)(rec + 4))[A] = (uint16_t)r;
     if (lane == 0) *(int*)rec = icur | (nacc << 16);
@@ -2114,11 +1976,7 @@ __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
 // ------------------------------------------------------------------------------------------------
 // reset (factory.py:134-148; global_entities.py:196-203; rules.py:182-199; SpawnEntity rules)
 // ------------------------------------------------------------------------------------------------
-#if MFG_RESET_INLINE  // inlined into k_reset / k_resetdone, so their register budget (waves_per_eu) applies to it
 __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scratch) {
-#else
-__device__ void env_reset(const Env& e, int* scratch) {
-#endif
   SpecP S = e.S;
   const int A = S->A, W = S->s.W;
   int reset_crash = 0;  // a reference exception inside reset(): reported by the next step (crashed + done)
@@ -2161,16 +2019,11 @@ __device__ void env_reset(const Env& e, int* scratch) {
       for (int b = 0; b < a; b++) occ |= rl(my_cell, b) == cell;
       return !occ;
     };
-#if MFG_RESET_DRAWS
     // the draws of shuffle(empty_positions) on the replay's branch-free chunked path; the first accepted draw
     // (i = m - 1) picks the slot pop() takes
     const int j = m < 2 ? (m == 1 ? 0 : -1)
                         : (S->replay_top14 ? replay_shuffle_t<true, false>(e, nullptr, m - 1)
                                            : replay_shuffle_t<false, false>(e, nullptr, m - 1));
-#else
-    const int j = mt_randbelow_seq<uint16_t>(e, m - 1, m - 1, nullptr);  // first Fisher-Yates step picks the last slot
-    if (m - 2 >= 1) mt_randbelow_seq<uint16_t>(e, m - 2, 1, nullptr);  // remaining draws of shuffle(empty_positions)
-#endif
     int k = 0, cell = -1;
     const int npos = S->s.n_positions[a];
     if (npos > 0) {
@@ -2660,11 +2513,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   const int agx = agp / W, agy = agp % W, orgx = org_l / W, orgy = org_l % W;
   // the first pass's rays are agent independent: loaded once per render, not once per agent, where the
   // registers they then hold across the agent loop do not cost occupancy (short rays, dense obs)
-#ifdef MFG_NO_RAY_HOIST  // measurement build: rays loaded per agent, ray words still prefetched
-  constexpr bool HOIST_RAYS = false;
-#else
-  constexpr bool HOIST_RAYS = MAXPTS <= 8 && (PK == 0 || (PK == 1 && MFG_PK1_HOIST));
-#endif
+  constexpr bool HOIST_RAYS = MAXPTS <= 8 && PK == 0;  // (packed renders: per agent, measured faster)
   constexpr bool PREFETCH_RS = MAXPTS <= 8 && PK != 2;
   RayLane<MAXPTS> ray0;
   if constexpr (HOIST_RAYS) ray0.load(S, lane);
@@ -2879,15 +2728,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     if (0)
 #endif
     for (int w0 = 0; w0 < dd; w0 += MFG_WAVE) {
-#if MFG_OBS_CLAMP
       // dense: lanes past the window repeat the last window cell (its value, to its address), so the layer
       // stores need no exec mask; packed mode keeps them out (its ballots count entries)
       const int wi = PK ? w0 + lane : min(w0 + lane, dd - 1);
       const bool inwin = PK ? wi < dd : true;
-#else
-      const int wi = w0 + lane;
-      const bool inwin = wi < dd;
-#endif
       // wi / d and wi % d through a float reciprocal (exact: (wi + 0.5) / d is >= 0.5 / d away from an integer
       // and the product's error is <= (wi + 0.5) / d * 2^-23, below that for wi < 2^22); the tests below are branch-free, every LDS
       // read has a valid clamped address and its result is masked
@@ -2998,10 +2842,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         // and k_obs 0.494 -> 0.543 ms, so it was dropped (k_obs).
 #if defined(MFG_ABLATE_OB_NOSTORE)  // timing only: the values are computed, (almost) never stored
         if (inwin && out == (OT)-12345.0) *op = out;
-#elif MFG_OBS_NT
-        if (inwin) __builtin_nontemporal_store(out, op);
 #else
-        if (inwin) *op = out;
+        if (inwin) __builtin_nontemporal_store(out, op);
 #endif
       }
     }
@@ -3044,11 +2886,7 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   e.setH(H_TOTAL_STEPS, e.H(H_TOTAL_STEPS) + 1);
   o.crashed = e.H(H_CRASHED);  // a crash the reset hit (or a crashed env stepped without a reset): done, no step
   wave_sync();
-#ifdef MFG_NO_PARLOGIC
-  const int a0 = 0;
-#else
   const int a0 = o.crashed ? A : act_parallel(e, my_act, o);
-#endif
   for (int a = a0; a < A && !o.crashed; a++) {
     if (uni(e.agpar()[a])) continue;  // paralyzed agents skip their action
     const int slot = rl(my_act, a);
@@ -3115,12 +2953,8 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
 #define MFG_WPB 4  // waves (envs) per workgroup at most; fewer when a slice is large (wpb_for)
 // k_logic<false, false> is SGPR-bound to 7 waves per SIMD (106 SGPRs); asking for 8 fits it in 78 SGPRs with one
 // SGPR spill (C3: 0.1505 -> 0.1303 ms per launch). The same request on the dense k_obs spills ~90 SGPRs into VGPR
-// lanes and made it slower (0.433 -> 0.451 ms), so k_obs keeps 7. MFG_NO_WPE drops the request.
-#ifndef MFG_NO_WPE
+// lanes and made it slower (0.433 -> 0.451 ms), so k_obs keeps 7.
 #define MFG_WPE_LOGIC(n) __attribute__((amdgpu_waves_per_eu(n)))
-#else
-#define MFG_WPE_LOGIC(n)
-#endif
 
 // full-record slice: [record][scratch][shuffle tables][BFS scratch if it fits]
 __device__ __forceinline__ void env_full(SpecP S, uint8_t* slice, Env& e, long long env) {
@@ -3275,7 +3109,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
 // Factory.reset(). A fixed grid of waves strides over the list (count <= B, every wave exits), so a step
 // with few episode ends costs a few waves instead of one wave per env.
 #ifndef MFG_OBS_UNIT  // host-unit kernel (not compiled in the render units)
-static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MFG_RESET_INLINE ? 4 : 1)))
+static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(4)))
 k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B, int rd_slot) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
@@ -3342,7 +3176,7 @@ __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* 
 // on the engine's second stream; null = none). With auto-reset, mfg_step renders the envs that did not finish
 // on the caller's stream while the finished ones are reset and rendered beside it.
 template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT>
-static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 ? (PK == 2 ? MFG_PK_WPE : 7) : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
+static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 ? 7 : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                       OT* obs, ObsPacked pk, const uint8_t* skip) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
@@ -3621,7 +3455,6 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_replay_done(const MfgDe
   const int wid = uni(threadIdx.x >> 6);
   const int32_t* lst = S->rd_list + (size_t)rd_slot * (size_t)(B + 2);
   const long long n = min((long long)uni(lst[0]), B);
-#if MFG_RPD_QUEUE
   // each wave's first env is its own index; after that the waves take entries nw, nw + 1, ... from a work queue
   // (lst[1] counts the entries taken, k_logic zeroes it with the count): debts differ per env, so a wave takes
   // its next env when it is done instead of a fixed stride. A step with few episode ends touches the counter
@@ -3637,14 +3470,6 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_replay_done(const MfgDe
     if (__lane_id() == 0) t = atomicAdd(taken, 1);
     q = nw + rl(t, 0);
   }
-#else
-  const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
-  for (long long q = (long long)blockIdx.x * (blockDim.x >> 6) + wid; q < n; q += nw) {
-    const long long env = uni(lst[2 + q]);
-    if (env < 0 || env >= B) continue;
-    replay_env(S, smem + (size_t)wid * S->lds_replay_per_wave, state + (size_t)env * S->L.size);
-  }
-#endif
 }
 #endif
 

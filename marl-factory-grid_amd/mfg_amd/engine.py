@@ -43,6 +43,8 @@ def load_lib():
     L = C.CDLL(str(LIB_PATH))
     L.mfg_create.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_void_p)]
     L.mfg_create.restype = C.c_int
+    L.mfg_create_variant.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.POINTER(C.c_void_p)]
+    L.mfg_create_variant.restype = C.c_int
     L.mfg_destroy.argtypes = [C.c_void_p]
     L.mfg_destroy.restype = C.c_int
     L.mfg_last_error.argtypes = [C.c_void_p]
@@ -85,10 +87,16 @@ def _check(rc, what, h=None):
         raise RuntimeError(f'{what} failed: {load_lib().mfg_last_error(h).decode()}')
 
 
-class Engine:
-    """B environments of one compiled spec on one GPU."""
+class MfgVariant(C.Structure):
+    """include/mfg.h mfg_variant: exact alternative code paths forced for the parity tests."""
+    _fields_ = [('shuffle_table_path', C.c_int32), ('full_temper', C.c_int32), ('bfs_hbm', C.c_int32),
+                ('pairs_lds', C.c_int32)]
 
-    def __init__(self, spec, n_envs, device=0):
+
+class Engine:
+    """B environments of one compiled spec on one GPU. variant: test-only {field: value} of mfg_variant."""
+
+    def __init__(self, spec, n_envs, device=0, variant=None):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError('mfg_amd.Engine needs a GPU (HIP); no CPU fallback exists')
@@ -99,7 +107,12 @@ class Engine:
         self.device = torch.device('cuda', device)
         torch.cuda.set_device(self.device)
         h = C.c_void_p()
-        _check(self.L.mfg_create(C.byref(spec.c), device, self.B, C.byref(h)), 'mfg_create')
+        if variant:
+            v = MfgVariant(**variant)
+            _check(self.L.mfg_create_variant(C.byref(spec.c), device, self.B, C.byref(v), C.byref(h)),
+                   'mfg_create_variant')
+        else:
+            _check(self.L.mfg_create(C.byref(spec.c), device, self.B, C.byref(h)), 'mfg_create')
         self.h = h
         lay = np.zeros(64, np.int32)
         n = self.L.mfg_layout(self.h, lay.ctypes.data_as(C.c_void_p))
