@@ -426,7 +426,21 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
   int first_j = -1;
+#ifndef MFG_RP_SINK
+#define MFG_RP_SINK 1
+#endif
+#ifndef MFG_RP_YWC
+#define MFG_RP_YWC 0
+#endif
+#ifndef MFG_RP_IW
+#define MFG_RP_IW 0
+#endif
+#if MFG_RP_SINK  // 128 B: one u16 per lane; lanes l and l + 32 share a dword: they sit in different lane groups of
+                 // the exchange, so the rejected lanes' sink edits of one group never hit the same dword
+  uint16_t* sink = (uint16_t*)e.scratch + (((lane & 31) << 1) | (lane >> 5));
+#else
   uint16_t* sink = (uint16_t*)e.scratch + lane;  // 128 B: one u16 per lane
+#endif
   uint32_t* ptab = e.stab;
   const int lo = 1;
   int idx = e.H(H_MT_IDX);
@@ -538,11 +552,19 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
       const uint32_t ad = (uint32_t)(uintptr_t)(acc ? &perm[j] : sink) & ~3u;
       asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(F) : "v"(ad), "v"(0xFFFFu << (sh & 31u)),
                    "v"((uint32_t)v << (sh & 31u)) : "memory");
+#if MFG_RP_YWC  // the next chunk's words loaded unconditionally from min(idxn, 560) (reloaded at the top if idxn > 560)
+      yw = mt[min(idxn, 560) + lane];
+#else
       if (idxn <= 560) yw = mt[idxn + lane];
+#endif
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F) : : "memory");
       asm("v_lshrrev_b32 %0, %1, %2" : "=v"(F) : "v"(sh), "v"(F));  // low 5 bits of sh; the i write keeps 16 bits
     }
+#if MFG_RP_IW  // rejected lanes write their sink instead of an exec-masked write
+    *(acc ? pi : sink) = (uint16_t)F;
+#else
     if (acc) *pi = (uint16_t)F;
+#endif
     wave_sync();
     }
 #else

@@ -37,13 +37,14 @@ class RecurrentAC(nn.Module):
     step-wise recurrent pass with episode restarts."""
 
     def __init__(self, observation_size, n_actions, obs_emb_size, action_emb_size, hidden_size_actor,
-                 hidden_size_critic, n_agents, use_agent_embedding=True, gru_window='cells'):
+                 hidden_size_critic, n_agents, use_agent_embedding=True, gru_window='fused'):
         super().__init__()
-        # how a window of T > 1 steps runs the GRUs: 'cells' = torch.gru_cell (one fused kernel) per step,
-        # 'segments' = one nn.GRU call over packed episode segments (_Segments). Measured on the MI355X (C3,
-        # B = 8,192, n_steps 5): 32.7 vs 102.3 ms per update (MIOpen's packed-sequence GRU), so 'cells'
-        if gru_window not in ('cells', 'segments'):
-            raise ValueError("gru_window must be 'cells' or 'segments'")
+        # how a window of T > 1 steps runs the GRUs: 'fused' = _GRUWindow (both GRUs, the window's GEMMs batched,
+        # forward and backward written out), 'cells' = torch.gru_cell (one fused kernel) per step and GRU under
+        # autograd, 'segments' = one nn.GRU call over packed episode segments (_Segments). Measured on the MI355X
+        # (C3, B = 8,192, n_steps 5): 'cells' 32.7 vs 'segments' 102.3 ms per update (MIOpen's packed-sequence GRU)
+        if gru_window not in ('fused', 'cells', 'segments'):
+            raise ValueError("gru_window must be 'fused', 'cells' or 'segments'")
         self.gru_window = gru_window
         observation_size = int(np.prod(observation_size))
         self.n_layers = 1
@@ -108,6 +109,13 @@ class RecurrentAC(nn.Module):
                                    self.gru_actor.bias_ih_l0, self.gru_actor.bias_hh_l0)[:, None]
             out_c = torch.gru_cell(mixed[:, 0], hc, self.gru_critic.weight_ih_l0, self.gru_critic.weight_hh_l0,
                                    self.gru_critic.bias_ih_l0, self.gru_critic.bias_hh_l0)[:, None]
+        elif self.gru_window == 'fused':  # a window: both GRUs in one autograd node, GEMMs batched over the window
+            keep = torch.ones((n, t), dtype=mixed.dtype, device=mixed.device) if starts is None else \
+                (~starts).to(mixed.dtype)
+            ga, gc = self.gru_actor, self.gru_critic
+            out_p, out_c = _GRUWindow.apply(mixed, keep, ha.detach(), hc.detach(), ga.weight_ih_l0, ga.weight_hh_l0,
+                                            ga.bias_ih_l0, ga.bias_hh_l0, gc.weight_ih_l0, gc.weight_hh_l0,
+                                            gc.bias_ih_l0, gc.bias_hh_l0)
         elif self.gru_window == 'segments':  # a window: one library RNN call per GRU over the episode segments
             seg = _Segments(starts, n, t, mixed.device)
             out_p = seg.run(self.gru_actor, mixed, ha)
@@ -216,6 +224,80 @@ class _EngineProj(torch.autograd.Function):
     def backward(ctx, g):
         idx, val = ctx.saved_tensors
         return None, None, _packed_weight_grad(idx, val, g, ctx.k).t(), g.sum(0), None
+
+
+class _GRUWindow(torch.autograd.Function):
+    """Both GRUs of RecurrentAC (layer 0, PyTorch gate order r, z, n) over a window of T steps with per-entry
+    restarts, forward and backward written out so the GEMMs are batched over the window:
+      forward:  the input gates of every step and both GRUs as ONE GEMM [N*T, I] x [I, 3Ha + 3Hc]; per step the
+                recurrent gates h W_hh^T (one GEMM per GRU, the only sequential part);
+      backward: per step the recurrent chain dh W_hh (one GEMM per GRU), then ONE GEMM each for the input-weight
+                gradient of both GRUs, the input gradient, and per GRU one recurrent-weight gradient over all N*T
+                rows (autograd over T fused cells issues 4 GEMMs per step and GRU: 48 instead of 10 at T = 6).
+    keep [N, T]: the state entering step s is h_{s-1} * keep[:, s] (0 = an episode restart at s). h0 gets no
+    gradient (the learner's carried state is detached, base_ac.py:126-128)."""
+
+    @staticmethod
+    def forward(ctx, x, keep, h0a, h0c, wia, wha, bia, bha, wic, whc, bic, bhc):
+        n, t, i_dim = x.shape
+        ha_dim, hc_dim = wha.shape[1], whc.shape[1]
+        wi = torch.cat([wia, wic], 0)  # [3Ha + 3Hc, I]
+        bi = torch.cat([bia, bic], 0)
+        gi = torch.addmm(bi, x.reshape(n * t, i_dim), wi.t()).view(n, t, -1)
+        outs, saved = [], []
+        for (h, wh, bh, lo, hd) in ((h0a, wha, bha, 0, ha_dim), (h0c, whc, bhc, 3 * ha_dim, hc_dim)):
+            hs, hps, rs, zs, ns, ghns = [], [], [], [], [], []
+            for s in range(t):
+                hp = h * keep[:, s:s + 1]
+                gh = torch.addmm(bh, hp, wh.t())
+                g = gi[:, s, lo:lo + 3 * hd]
+                r = torch.sigmoid(g[:, :hd] + gh[:, :hd])
+                z = torch.sigmoid(g[:, hd:2 * hd] + gh[:, hd:2 * hd])
+                ghn = gh[:, 2 * hd:]
+                nn_ = torch.tanh(g[:, 2 * hd:] + r * ghn)
+                h = nn_ + z * (hp - nn_)  # (1 - z) n + z h
+                hs.append(h); hps.append(hp); rs.append(r); zs.append(z); ns.append(nn_); ghns.append(ghn)
+            outs.append(torch.stack(hs, 1))
+            saved += [torch.stack(v, 1) for v in (hps, rs, zs, ns, ghns)]
+        ctx.save_for_backward(x, keep, wi, wha, whc, *saved)
+        ctx.dims = (ha_dim, hc_dim)
+        return outs[0], outs[1]
+
+    @staticmethod
+    def backward(ctx, douta, doutc):
+        x, keep, wi, wha, whc, *saved = ctx.saved_tensors
+        ha_dim, hc_dim = ctx.dims
+        n, t, i_dim = x.shape
+        dgis, grads = [], []
+        for gi_idx, (dout, wh, hd) in enumerate(((douta, wha, ha_dim), (doutc, whc, hc_dim))):
+            hps, rs, zs, ns, ghns = saved[5 * gi_idx:5 * gi_idx + 5]
+            dgi = torch.empty((n, t, 3 * hd), dtype=x.dtype, device=x.device)
+            dgh = torch.empty_like(dgi)
+            carry = torch.zeros((n, hd), dtype=x.dtype, device=x.device)
+            for s in range(t - 1, -1, -1):
+                dh = carry if dout is None else dout[:, s] + carry
+                r, z, nn_, ghn, hp = rs[:, s], zs[:, s], ns[:, s], ghns[:, s], hps[:, s]
+                dn = dh * (1.0 - z) * (1.0 - nn_ * nn_)
+                dz = dh * (hp - nn_) * z * (1.0 - z)
+                dr = dn * ghn * r * (1.0 - r)
+                dgi[:, s, :hd] = dr
+                dgi[:, s, hd:2 * hd] = dz
+                dgi[:, s, 2 * hd:] = dn
+                dgh[:, s, :hd] = dr
+                dgh[:, s, hd:2 * hd] = dz
+                dgh[:, s, 2 * hd:] = dn * r
+                dhp = torch.addmm(dh * z, dgh[:, s], wh)  # dh z + dgh W_hh
+                carry = dhp * keep[:, s:s + 1]
+            dgis.append(dgi)
+            dgh2 = dgh.reshape(n * t, 3 * hd)
+            grads.append((dgh2.t() @ hps.reshape(n * t, hd), dgh2.sum(0)))  # dW_hh, db_hh
+        dgi_all = torch.cat(dgis, 2).reshape(n * t, -1)
+        dwi = dgi_all.t() @ x.reshape(n * t, i_dim)  # [3Ha + 3Hc, I]
+        dbi = dgi_all.sum(0)
+        dx = (dgi_all @ wi).view(n, t, i_dim)
+        sa = 3 * ha_dim
+        return (dx, None, None, None, dwi[:sa], grads[0][0], dbi[:sa], grads[0][1],
+                dwi[sa:], grads[1][0], dbi[sa:], grads[1][1])
 
 
 def _gru_cell(gi, h, gru):

@@ -245,3 +245,27 @@ def test_windowed_gru_segments_match_the_step_loop():
     g2 = torch.autograd.grad(ref.square().sum(), [x, gru.weight_hh_l0])
     for a, b in zip(g1, g2):
         assert torch.allclose(a, b, atol=1e-4, rtol=1e-4)
+
+
+def test_fused_gru_window_matches_cells():
+    """gru_window 'fused' (_GRUWindow: both GRUs, batched window GEMMs, hand-written backward) equals the
+    per-step torch.gru_cell loop under autograd: outputs and every parameter gradient, with restarts."""
+    torch.manual_seed(3)
+    N, T = 5, 6
+    nets = {m: RecurrentAC((2, 3, 3), 7, 12, 4, 8, 6, N, use_agent_embedding=False, gru_window=m)
+            for m in ('fused', 'cells')}
+    nets['cells'].load_state_dict(nets['fused'].state_dict())
+    emb = torch.randn(N, T, 12)
+    acts = torch.randint(-1, 7, (N, T))
+    ha, hc = torch.randn(N, 1, 8), torch.randn(N, 1, 6)
+    starts = torch.rand(N, T) < 0.25
+    res = {}
+    for m, net in nets.items():
+        out = net.forward_emb(emb, acts, ha, hc, agent_ids=torch.arange(N), starts=starts)
+        (out['logits'].square().sum() + out['critic'].sin().sum()).backward()
+        res[m] = (out, {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None})
+    for k in ('logits', 'critic', 'hidden_actor', 'hidden_critic'):
+        assert torch.allclose(res['fused'][0][k], res['cells'][0][k], rtol=1e-5, atol=1e-6), k
+    assert res['fused'][1].keys() == res['cells'][1].keys()
+    for k, g in res['cells'][1].items():
+        assert torch.allclose(res['fused'][1][k], g, rtol=1e-4, atol=1e-6), (k, (res['fused'][1][k] - g).abs().max())
