@@ -2865,7 +2865,14 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
 #if defined(MFG_ABLATE_OB_NOSTORE)  // timing only: the values are computed, (almost) never stored
         if (inwin && out == (OT)-12345.0) *op = out;
 #else
-        if (inwin) __builtin_nontemporal_store(out, op);
+#ifndef MFG_OBS_NT64
+#define MFG_OBS_NT64 1
+#endif
+        if (sizeof(OT) == 8 && !MFG_OBS_NT64) {  // f64 rows (392 B at C3): plain stores, merged into whole lines in L2
+          if (inwin) *op = out;
+        } else {
+          if (inwin) __builtin_nontemporal_store(out, op);
+        }
 #endif
       }
     }
