@@ -268,11 +268,11 @@ static int validate_spec(const mfg_spec* s) {
   if (s->n_floor < 1 || s->n_floor > s->H * s->W || !s->floor_cells) return fail("n_floor out of range");
   if (s->n_walls < 0 || s->n_walls > s->H * s->W) return fail("n_walls out of range");
   // the ray radius is the window diameter (Q13): 2 r + 1, or min(H, W) with full observability; a ray holds
-  // radius + 1 points and the walk keeps them in 32-bit masks (the per-agent tables must also fit the LDS,
-  // checked below)
-  if (s->pomdp_r < 0 || s->pomdp_r > 15) return fail("engine supports pomdp_r in [0, 15] (rays of <= 32 points)");
-  if (s->pomdp_r == 0 && std::min(s->H, s->W) > 31)
-    return fail("full observability (pomdp_r 0) needs min(H, W) <= 31 (rays of <= 32 points)");
+  // radius + 1 points and the walk keeps them in one 32- or 64-bit mask (the per-agent tables must also fit the
+  // LDS, checked below)
+  if (s->pomdp_r < 0 || s->pomdp_r > 31) return fail("engine supports pomdp_r in [0, 31] (rays of <= 64 points)");
+  if (s->pomdp_r == 0 && std::min(s->H, s->W) > 63)
+    return fail("full observability (pomdp_r 0) needs min(H, W) <= 63 (rays of <= 64 points)");
   for (int a = 0; a < s->n_agents; a++) {
     if (s->n_positions[a] < 0 || s->n_positions[a] > MFG_MAX_POSITIONS) return fail("n_positions out of range");
     for (int k = 0; k < s->n_positions[a]; k++)

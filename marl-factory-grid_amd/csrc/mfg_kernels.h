@@ -403,12 +403,21 @@ __device__ __forceinline__ uint32_t lds_xchg_u16_wait(uint32_t old, uint16_t* p)
 #define RP_STAB_N 65
 #define RP_HDR_N 8  // header ints k_replay keeps in its slice (H_DEBT, H_MT_IDX)
 static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice");
+#ifndef MFG_RP_BAND
+#define MFG_RP_BAND 0
+#endif
+#ifndef MFG_RP_BR
+#define MFG_RP_BR 0
+#endif
 #ifndef RP_SERIAL_FWD
 #define RP_SERIAL_FWD 4  // blocks with at most this many forwards resolve them serially (no LDS table)
 #endif
 // The chunk's acceptance fixed point: from the seed m, iterate m = ballot(mbcnt(m) <= c) until it is stable;
 // returns A = mbcnt(m) (#accepted lanes below this one) and leaves the accepted set in m.
 __device__ __forceinline__ int accept_ranks(u64& m, int c) {
+#if MFG_RP_BR & 1  // two rounds before the first stability test (92% of chunks need two): one loop branch less per chunk
+  m = ballot(mbcnt(m) <= c);
+#endif
   for (;;) {
     const int A = mbcnt(m);
     const u64 m2 = ballot(A <= c);
@@ -454,6 +463,13 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   // words are already in yw follows from idx alone (a twisted state had idx >= 624 > 560).
   uint32_t yw = idx <= 560 ? mt[idx + lane] : 0u;
   const int lane34 = (3 * lane) >> 2;
+#if MFG_RP_BAND
+  // the width band kept across chunks: sh = 32 - k (k = bitlen(icur + 1)) and its lowest i, blo = max(lo, 2^(k-1) - 1);
+  // both change only where a chunk fills its band (nacc = span + 1, i.e. inext < blo), which is also the only case
+  // where fewer than 64 words are consumed: one scalar test per chunk instead of the width and consumed arithmetic
+  int sh = __clz(icur + 1);
+  int blo = max(lo, (int)(0x80000000u >> sh) - 1);
+#endif
   while (icur >= lo) {
     if (idx > 560) {
       if (idx >= 624) {
@@ -471,14 +487,21 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
         yw = jw < 624 ? mt[jw < 624 ? jw : 0] : nw;
       }
     }
+#if MFG_RP_BR & 2  // the chunks between two refills: one exit test per chunk (the shuffle's end or the state's refill)
+    for (;;) {
+#endif
     const uint32_t y = TOP14 ? mt_temper3(yw) : mt_temper(yw);
     // One bit width per chunk: k = bitlen(icur + 1), and the chunk stops where bitlen(i + 1) would
     // change (i < 2^(k-1) - 1) or at lo. Within it accept <=> A <= c = min(icur - r, span), with
     // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
     // start the next chunk). So every chunk takes the same branch-free path, power-of-two crossings
     // and the i < 64 tail included.
+#if MFG_RP_BAND
+    const int span = icur - blo;  // highest rank at width k
+#else
     const int sh = __clz(icur + 1);
     const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
+#endif
     uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from a seed at A_l ~ 3l/4 (the mean acceptance; 1.91 rounds per
@@ -493,8 +516,20 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     const int nacc = popc(m);
     // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1), and then
     // exactly the lanes up to the last accepted one (scalar, no vector compare)
+#if MFG_RP_BAND
+    const int inext = icur - nacc;
+    int consumed = 64;
+    if (__builtin_expect(inext < blo, 0)) {  // the band filled: the chunk ends it; the next chunk starts the next band
+      asm volatile("; band end" ::);  // a real branch: the compiler would otherwise compute the rare path every chunk
+      consumed = 64 - __builtin_clzll(m);
+      sh = __clz(inext + 1);
+      blo = max(lo, (int)(0x80000000u >> sh) - 1);
+    }
+    const int idxn = idx + consumed;
+#else
     const int consumed = nacc > span ? 64 - __builtin_clzll(m) : 64;
     const int inext = icur - nacc, idxn = idx + consumed;
+#endif
 #ifndef MFG_ABLATE_NOSWAP
     if constexpr (!SWAP) {
       if (first_j < 0 && m) first_j = rl((int)r, ffs64(m));
@@ -516,6 +551,12 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     u64 cm = ballot(j > inext) & ballot(j < i) & m;
 #ifdef MFG_ABLATE_NOFWD
     cm = 0;
+#endif
+#ifdef MFG_ABLATE_NOFWD_SERIAL  // timing only: chunks with few forwards skip them
+    if (popc(cm) <= RP_SERIAL_FWD) cm = 0;
+#endif
+#ifdef MFG_ABLATE_NOFWD_TABLE  // timing only: chunks with many forwards skip them
+    if (popc(cm) > RP_SERIAL_FWD) cm = 0;
 #endif
     if (cm) {
       if (popc(cm) <= RP_SERIAL_FWD) {
@@ -552,7 +593,7 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
       const uint32_t ad = (uint32_t)(uintptr_t)(acc ? &perm[j] : sink) & ~3u;
       asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(F) : "v"(ad), "v"(0xFFFFu << (sh & 31u)),
                    "v"((uint32_t)v << (sh & 31u)) : "memory");
-#if MFG_RP_YWC  // the next chunk's words loaded unconditionally from min(idxn, 560) (reloaded at the top if idxn > 560)
+#if MFG_RP_YWC || (MFG_RP_BR & 2)  // the next chunk's words loaded unconditionally from min(idxn, 560) (reloaded at the top if idxn > 560)
       yw = mt[min(idxn, 560) + lane];
 #else
       if (idxn <= 560) yw = mt[idxn + lane];
@@ -572,6 +613,10 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
 #endif
     icur = inext;
     idx = idxn;
+#if MFG_RP_BR & 2
+    if (__builtin_expect(((icur - lo) | (560 - idx)) < 0, 0)) break;  // icur < lo or idx > 560: one sign test
+    }
+#endif
   }
   if (idx > 624) {  // words of the next state were consumed: make the state canonical (CPython's mti)
     mt_twist(e);

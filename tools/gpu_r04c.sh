@@ -3,7 +3,7 @@
 # paths), the 2-rank shared-GPU bench and the A2C loop.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_ranks.py tests/test_gpu_timed_path.py tests/test_gpu_parity.py \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_ranks.py tests/test_gpu_timed_path.py tests/test_gpu_parity.py tests/test_marl.py \
   -m gpu -v --timeout 800 --timeout-method thread > gpurun_out/r04b_tests.log 2>&1 || { tail -40 gpurun_out/r04b_tests.log; exit 1; }
 tail -3 gpurun_out/r04b_tests.log
 MFG_BENCH_SHARE_GPU=1 timeout -k 10 400 python bench.py --gpus 2 --backend gloo --warmup 600 --steps 400 \
