@@ -947,7 +947,16 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
                        ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
                        auto_reset, e->rd_slot);
     } else if (e->h.step_rng) {
-    hipLaunchKernelGGL((k_logic<true, false>), GEOMW(e->h.lds_logic, logic_wpb), st,
+    // RespawnDirt is the only in-step RNG consumer here: the envs without a spawn this step run the lean step at
+    // its occupancy, the few with one (C4 ~1/16) the full-record step
+    const int lean_lds = e->h.L.o_logic + 4 * MFG_WAVE;
+    hipLaunchKernelGGL((k_logic<false, false, 1>), GEOMW(lean_lds, logic_wpb), st,
+                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
+                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
+                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
+                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
+                       auto_reset, e->rd_slot);
+    hipLaunchKernelGGL((k_logic<true, false, 2>), GEOMW(e->h.lds_logic, logic_wpb), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,

@@ -3110,7 +3110,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec*
 // One env-step of every env (no reset, no render). FULL: the spec consumes the floor order inside a
 // step (S->step_rng), so the whole record incl. MT/perm is staged; otherwise only the lean prefix.
 #ifndef MFG_OBS_UNIT  // host-unit kernel (not compiled in the render units)
-template <bool FULL, bool MAINT>
+template <bool FULL, bool MAINT, int SEL = 0>
 static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAINT ? 1 : 8) k_logic(const MfgDevSpec* S_, uint8_t* state, long long B,
                                                         const int32_t* actions, unsigned philox_seed,
                                                         unsigned env_base, long long step, double* reward,
@@ -3121,6 +3121,22 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   const int wid = threadIdx.x >> 6;  // (a uniform wid here measured slower: 0.319 vs 0.298 ms at C3)
   const long long env = (long long)blockIdx.x * (blockDim.x >> 6) + wid;
   if (env >= B) return;
+  // SEL (specs whose only in-step RNG consumer is RespawnDirt): 1 = the envs where no spawn fires this step (the
+  // lean k_logic<false, false, 1>, launched first), 2 = the envs where one fires (k_logic<true, false, 2>, after
+  // it); 0 = every env. A spawn fires exactly when its rule counter is 0 at the start of the step
+  // (clean_up/rules.py:49-59). The first launch has already stepped (and counted down) the other envs when the
+  // second runs, so it marks the envs it leaves in rd_flag (2), which the second takes and overwrites.
+  if constexpr (SEL == 1) {
+    const int* rc = (const int*)(state + (size_t)env * S->L.size + S->L.o_rule_ctr);
+    bool fire = false;
+    for (uint32_t m = S->respawn_mask; m; m &= m - 1) fire |= uni(rc[__ffs(m) - 1]) == 0;
+    if (fire) {
+      if (lane_id() == 0) S->rd_flag[env] = 2;
+      return;
+    }
+  } else if constexpr (SEL == 2) {
+    if (uni((int)S->rd_flag[env]) != 2) return;
+  }
   Env e;
   uint8_t* slice = smem + (size_t)wid * S->lds_logic;
   constexpr bool full = FULL;
@@ -3131,10 +3147,15 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
   }
   uint8_t* rec = state + (size_t)env * S->L.size;
-  const int bytes = full ? S->L.size : S->L.o_logic;
+  // FULL without maintainers: a RespawnDirt rule is the only in-step reader of the MT state and the floor order, and
+  // it spawns exactly when its counter is 0 at the start of the step (clean_up/rules.py:49-59; nothing else changes
+  // the counter before its tick). So only the lean prefix is staged, and the MT/perm tail only in the envs where a
+  // spawn fires (k_replay_sel paid their earlier debt): C4 ~1/16 of the envs per step.
+  constexpr bool lazy = FULL && !MAINT;
+  const int bytes = full && !lazy ? S->L.size : S->L.o_logic;
   // lean records of <= 1 KiB: each lane keeps its 16-B chunk and writes it back only if the step changed it
   // (most of the record is per-episode constant: frozen origins, ids, counters of idle rules)
-  const bool one_pass = !full && (bytes >> 4) <= MFG_WAVE;
+  const bool one_pass = (!full || lazy) && (bytes >> 4) <= MFG_WAVE;
   uint4 orig = make_uint4(0, 0, 0, 0);
   if (one_pass && e.lane < (bytes >> 4)) orig = ((const uint4*)rec)[e.lane];
   // the actions (a buffer load or Philox) while the record load is in flight
@@ -3154,6 +3175,16 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     rec_copy(e.lds, rec, bytes, e.lane);
   }
   wave_sync();
+  // the RNG tail [o_mt, o_mstate) rounded to 16 B (o_mt is 16-B aligned; the rounding stays inside the record)
+  const int o_tail = S->L.o_mt, n_tail = (S->L.o_mstate - S->L.o_mt + 15) & ~15;
+  bool rng_tail = false;
+  if constexpr (lazy) {
+    for (uint32_t m = S->respawn_mask; m; m &= m - 1) rng_tail |= uni(e.rctr()[__ffs(m) - 1]) == 0;
+    if (rng_tail) {
+      rec_copy(e.lds + o_tail, rec + o_tail, n_tail, e.lane);
+      wave_sync();
+    }
+  }
   StepOut o;
   env_step<FULL, MAINT>(e, my_act, o, e.scratch);
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
@@ -3176,6 +3207,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   } else {
     rec_copy(rec, e.lds, bytes, e.lane);
   }
+  if (lazy && rng_tail) rec_copy(rec + o_tail, e.lds + o_tail, n_tail, e.lane);
 }
 #endif
 
