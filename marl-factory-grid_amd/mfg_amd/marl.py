@@ -32,6 +32,67 @@ import torch.nn.functional as F
 from torch.distributions import Categorical
 
 
+SPLIT_ROWS = 2048  # rows per split of a tall-K weight-gradient GEMM (_tall_tn)
+
+
+def _tall_tn(a, b, rows=None):
+    """a^T @ b for tall a [K, m], b [K, n] (weight gradients over N*T rows: K ~ 393K, m x n ~ 100 x 100). As one
+    GEMM the library tiles only the small m x n output (a handful of workgroups walking all of K: ~1 ms each on the
+    MI355X at C3's learner); split into K / rows batched GEMMs (one workgroup set per split) and summed it fills the
+    chip. Same products, different summation order (fp32 rounding only)."""
+    rows = rows or SPLIT_ROWS
+    k = a.shape[0]
+    s = k // rows
+    if s < 2:
+        return a.t() @ b
+    k0 = s * rows
+    out = torch.bmm(a[:k0].reshape(s, rows, -1).transpose(1, 2), b[:k0].reshape(s, rows, -1)).sum(0)
+    if k0 < k:
+        out = out + a[k0:].t() @ b[k0:]
+    return out
+
+
+class _Linear(torch.autograd.Function):
+    """x @ w^T + b on [M, in] rows with the weight gradient by _tall_tn (nn.Linear's backward is one tall-K GEMM)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        return g @ w, _tall_tn(g, x), g.sum(0)
+
+
+def _lin(mod, x):
+    """mod (nn.Linear) applied to x [..., in] through _Linear (same parameters)."""
+    lead = x.shape[:-1]
+    return _Linear.apply(x.reshape(-1, x.shape[-1]), mod.weight, mod.bias).view(*lead, -1)
+
+
+class _Embed(torch.autograd.Function):
+    """nn.Embedding lookup whose weight gradient is onehot(idx)^T @ g by _tall_tn: the embedding's own backward
+    scatters M rows onto a table of ~10 rows (action embedding), serialised on the few hot rows."""
+
+    @staticmethod
+    def forward(ctx, idx, w, padding_idx):
+        ctx.save_for_backward(idx)
+        ctx.n, ctx.pad = w.shape[0], padding_idx
+        return w[idx]
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        oh = F.one_hot(idx.reshape(-1), ctx.n).to(g2.dtype)
+        gw = _tall_tn(oh, g2)
+        if ctx.pad is not None:
+            gw[ctx.pad] = 0  # nn.Embedding(padding_idx): that row gets no gradient
+        return None, gw, None
+
+
 class RecurrentAC(nn.Module):
     """``algorithms/marl/networks.py:7-69`` with the same parameters; adds the packed-obs projection and a
     step-wise recurrent pass with episode restarts."""
@@ -94,14 +155,20 @@ class RecurrentAC(nn.Module):
         """obs_emb [N, T, E] (obs_proj output), actions [N, T] (last action, -1 = none), hidden [N, 1, H].
         starts [N, T] bool: the recurrent state restarts from zero at these entries (episode starts)."""
         n, t = obs_emb.shape[:2]
-        action_emb = self.action_emb(actions + 1)  # shift by one: padding idx (networks.py:53)
+        # learner windows with grad: the same layers with their weight gradients as split-K GEMMs (_tall_tn)
+        sk = t > 1 and torch.is_grad_enabled()
+        action_emb = _Embed.apply(actions + 1, self.action_emb.weight, self.action_emb.padding_idx) if sk else \
+            self.action_emb(actions + 1)  # shift by one: padding idx (networks.py:53)
         if not self.use_agent_embedding:
             x_t = torch.cat((obs_emb, action_emb), -1)
         else:
             ids = agent_ids if agent_ids is not None else torch.arange(n, device=obs_emb.device)
             agent_emb = self.agent_emb(ids.view(-1, 1).expand(n, t))
             x_t = torch.cat((obs_emb, agent_emb, action_emb), -1)
-        mixed = self.mix(x_t)
+        if sk:
+            mixed = _lin(self.mix[3], torch.tanh(_lin(self.mix[1], torch.tanh(x_t))))
+        else:
+            mixed = self.mix(x_t)
         ha = hidden_actor[:, 0]
         hc = hidden_critic[:, 0]
         if t == 1 and (starts is None or not bool(starts.any())):  # acting: one fused cell per GRU
@@ -134,8 +201,12 @@ class RecurrentAC(nn.Module):
                 ps.append(ha)
                 cs.append(hc)
             out_p, out_c = torch.stack(ps, 1), torch.stack(cs, 1)
-        logits = self.action_head(out_p)
-        critic = self.critic_head(out_c).squeeze(-1)
+        if sk:
+            logits = _lin(self.action_head[2], torch.tanh(_lin(self.action_head[0], out_p)))
+            critic = _lin(self.critic_head[2], torch.tanh(_lin(self.critic_head[0], out_c))).squeeze(-1)
+        else:
+            logits = self.action_head(out_p)
+            critic = self.critic_head(out_c).squeeze(-1)
         return dict(logits=logits, critic=critic, hidden_actor=out_p, hidden_critic=out_c)
 
 
@@ -205,8 +276,23 @@ def _packed_weight_grad(idx, val, g, k):
     for r0 in range(0, idx.shape[0], step):
         d = torch.zeros((min(step, idx.shape[0] - r0), k), dtype=g.dtype, device=g.device)
         d.scatter_add_(1, idx[r0:r0 + step], val[r0:r0 + step].to(g.dtype))
-        gw.addmm_(d.t(), g[r0:r0 + step])
+        gw += _tall_tn(d, g[r0:r0 + step])
     return gw
+
+
+def _project_dense(idx, val, proj):
+    """obs_proj over packed rows without grad: the rows scattered to dense blocks (<= 512 MiB) and one GEMM each
+    (embedding_bag with per-sample weights ran 0.77 ms for C3's 65,536 rows on the MI355X)."""
+    lead, cap = idx.shape[:-1], idx.shape[-1]
+    idx2, val2 = idx.reshape(-1, cap).long(), val.reshape(-1, cap)
+    k = proj.weight.shape[1]
+    out = torch.empty((idx2.shape[0], proj.weight.shape[0]), dtype=proj.weight.dtype, device=idx2.device)
+    step = max(1, (1 << 27) // max(k, 1))
+    for r0 in range(0, idx2.shape[0], step):
+        d = torch.zeros((min(step, idx2.shape[0] - r0), k), dtype=proj.weight.dtype, device=idx2.device)
+        d.scatter_add_(1, idx2[r0:r0 + step], val2[r0:r0 + step].to(d.dtype))
+        torch.addmm(proj.bias, d, proj.weight.t(), out=out[r0:r0 + step])
+    return out.view(*lead, -1)
 
 
 class _EngineProj(torch.autograd.Function):
@@ -224,6 +310,35 @@ class _EngineProj(torch.autograd.Function):
     def backward(ctx, g):
         idx, val = ctx.saved_tensors
         return None, None, _packed_weight_grad(idx, val, g, ctx.k).t(), g.sum(0), None
+
+
+_GRU_LIB = None
+
+
+def _gru_lib():
+    """libmfg_hip.so's learner kernels (include/mfg_learn.h), bound once."""
+    global _GRU_LIB
+    if _GRU_LIB is None:
+        import ctypes as C
+        from .engine import load_lib
+        L = load_lib()
+        p, i64 = C.c_void_p, C.c_int64
+        L.mfg_gru_fwd_step.argtypes = [p, i64, p, p, p, i64, p, i64, p, i64, p, p, p, p, p, i64, i64, C.c_int, p]
+        L.mfg_gru_fwd_step.restype = C.c_int
+        L.mfg_gru_bwd_step.argtypes = [p, i64, p, p, i64, p, p, p, p, p, i64, p, i64, p, i64, p, i64, C.c_int, p]
+        L.mfg_gru_bwd_step.restype = C.c_int
+        _GRU_LIB = L
+    return _GRU_LIB
+
+
+def _use_gru_kernels(x):
+    """The learner's GRU window runs its elementwise steps as HIP kernels on the GPU (fp32); CPU tensors take the
+    tensor code (the same formulas)."""
+    return x.is_cuda and x.dtype == torch.float32
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
 
 
 class _GRUWindow(torch.autograd.Function):
@@ -245,6 +360,30 @@ class _GRUWindow(torch.autograd.Function):
         bi = torch.cat([bia, bic], 0)
         gi = torch.addmm(bi, x.reshape(n * t, i_dim), wi.t()).view(n, t, -1)
         outs, saved = [], []
+        if _use_gru_kernels(x):  # per step: the recurrent GEMM + one fused elementwise kernel (mfg_gru_fwd_step)
+            L, st = _gru_lib(), torch.cuda.current_stream(x.device).cuda_stream
+            keep = keep.contiguous()
+            g_all = gi.shape[-1]
+            for (h, wh, bh, lo, hd) in ((h0a, wha, bha, 0, ha_dim), (h0c, whc, bhc, 3 * ha_dim, hc_dim)):
+                hs = torch.empty((n, t, hd), dtype=x.dtype, device=x.device)
+                sv = torch.empty((5, n, t, hd), dtype=x.dtype, device=x.device)  # hp, r, z, n, gh_n
+                bh = bh.contiguous()
+                hcur, h_row = h.contiguous(), hd
+                for s in range(t):
+                    gh0 = hcur @ wh.t()
+                    rc = L.mfg_gru_fwd_step(gi[:, s, lo:].data_ptr(), t * g_all, gh0.data_ptr(), bh.data_ptr(),
+                                            hcur.data_ptr(), h_row, keep[:, s].data_ptr(), t, hs[:, s].data_ptr(),
+                                            t * hd, sv[0, :, s].data_ptr(), sv[1, :, s].data_ptr(),
+                                            sv[2, :, s].data_ptr(), sv[3, :, s].data_ptr(), sv[4, :, s].data_ptr(),
+                                            t * hd, n, hd, st)
+                    if rc:
+                        raise RuntimeError('mfg_gru_fwd_step failed')
+                    hcur, h_row = hs[:, s], t * hd
+                outs.append(hs)
+                saved += list(sv.unbind(0))
+            ctx.save_for_backward(x, keep, wi, wha, whc, *saved)
+            ctx.dims = (ha_dim, hc_dim)
+            return outs[0], outs[1]
         for (h, wh, bh, lo, hd) in ((h0a, wha, bha, 0, ha_dim), (h0c, whc, bhc, 3 * ha_dim, hc_dim)):
             hs, hps, rs, zs, ns, ghns = [], [], [], [], [], []
             for s in range(t):
@@ -269,8 +408,31 @@ class _GRUWindow(torch.autograd.Function):
         ha_dim, hc_dim = ctx.dims
         n, t, i_dim = x.shape
         dgis, grads = [], []
+        gpu = _use_gru_kernels(x)
         for gi_idx, (dout, wh, hd) in enumerate(((douta, wha, ha_dim), (doutc, whc, hc_dim))):
             hps, rs, zs, ns, ghns = saved[5 * gi_idx:5 * gi_idx + 5]
+            if gpu:  # per step: one fused elementwise kernel (mfg_gru_bwd_step) + the recurrent GEMM
+                L, st = _gru_lib(), torch.cuda.current_stream(x.device).cuda_stream
+                dgi = torch.empty((n, t, 3 * hd), dtype=x.dtype, device=x.device)
+                dgh = torch.empty_like(dgi)
+                dout = None if dout is None else dout.contiguous()
+                sv_row = hps.stride(0)
+                dhp = None
+                for s in range(t - 1, -1, -1):
+                    dhz = torch.empty((n, hd), dtype=x.dtype, device=x.device)
+                    rc = L.mfg_gru_bwd_step(None if dout is None else dout[:, s].data_ptr(), t * hd, _ptr(dhp),
+                                            None if dhp is None else keep[:, s + 1].data_ptr(), t,
+                                            rs[:, s].data_ptr(), zs[:, s].data_ptr(), ns[:, s].data_ptr(),
+                                            ghns[:, s].data_ptr(), hps[:, s].data_ptr(), sv_row,
+                                            dgi[:, s].data_ptr(), t * 3 * hd, dgh[:, s].data_ptr(), t * 3 * hd,
+                                            dhz.data_ptr(), n, hd, st)
+                    if rc:
+                        raise RuntimeError('mfg_gru_bwd_step failed')
+                    dhp = torch.addmm(dhz, dgh[:, s], wh)
+                dgis.append(dgi)
+                dgh2 = dgh.reshape(n * t, 3 * hd)
+                grads.append((_tall_tn(dgh2, hps.reshape(n * t, hd)), dgh2.sum(0)))
+                continue
             dgi = torch.empty((n, t, 3 * hd), dtype=x.dtype, device=x.device)
             dgh = torch.empty_like(dgi)
             carry = torch.zeros((n, hd), dtype=x.dtype, device=x.device)
@@ -290,9 +452,9 @@ class _GRUWindow(torch.autograd.Function):
                 carry = dhp * keep[:, s:s + 1]
             dgis.append(dgi)
             dgh2 = dgh.reshape(n * t, 3 * hd)
-            grads.append((dgh2.t() @ hps.reshape(n * t, hd), dgh2.sum(0)))  # dW_hh, db_hh
+            grads.append((_tall_tn(dgh2, hps.reshape(n * t, hd)), dgh2.sum(0)))  # dW_hh, db_hh
         dgi_all = torch.cat(dgis, 2).reshape(n * t, -1)
-        dwi = dgi_all.t() @ x.reshape(n * t, i_dim)  # [3Ha + 3Hc, I]
+        dwi = _tall_tn(dgi_all, x.reshape(n * t, i_dim))  # [3Ha + 3Hc, I]
         dbi = dgi_all.sum(0)
         dx = (dgi_all @ wi).view(n, t, i_dim)
         sa = 3 * ha_dim
@@ -485,7 +647,7 @@ class BatchedA2C:
             self.h0a, self.h0c = self.ha.clone(), self.hc.clone()
             # new weights: the engine projects with them from now on; o_0's projection is redone here
             self.pobs.set_projection(self.net.obs_proj.weight, self.net.obs_proj.bias)
-            self.pobs.emb[0].copy_(self.net.project_packed(self.pobs.idx[0], self.pobs.val[0]))
+            self.pobs.emb[0].copy_(_project_dense(self.pobs.idx[0], self.pobs.val[0], self.net.obs_proj))
         self.t = 0
 
     def train(self, n_updates):
