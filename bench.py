@@ -46,7 +46,6 @@ PARITY_TESTS = {  # the GPU tests that pin the exact mode each line times (tests
     'f32': 'tests/test_gpu_timed_path.py::test_timed_path_k8_fp32_b65536_matches_oracle'}
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CU_CLOCK_HZ, N_CU = 2.4e9, 256   # MI355X: 256 CUs, 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
-BOX_CPU_SHARE = 16               # host cores the GPU box allots one GPU (worker pools are sized to it)
 METRIC = "env-steps/sec (whole node), 8-agent 'large' level, batch 65536, 1/2/4/8 MI355X"
 
 
@@ -98,6 +97,15 @@ def algo_bytes(kernel, spec, obs_bytes_per_env, k_launch):
     if kernel == 'k_replay':
         return 2 * (4 * 624 + 2 * spec.c.n_floor)  # MT state + floor permutation, read + written
     return None
+
+
+def cgroup_cpus():
+    """CPUs the cgroup v2 quota allows (cpu.max 'quota period'), or None without a quota."""
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        return None if q == 'max' else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(config, seconds, workers, seed):
@@ -322,7 +330,7 @@ def main():
     ap.add_argument('--config', default='large8.yaml')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--cpu-workers', type=int, default=0,
-                    help='0 = min(16, affinity cores): the GPU box allots 16 host cores per GPU')
+                    help='0 = the usable cores: min(affinity, cgroup cpu.max quota)')
     ap.add_argument('--obs-dtype', choices=['f32', 'f64'], default='f64',
                     help='obs precision of the headline line: f64, the reference\'s own (Q25, '
                          'utils/observation_builder.py:162); f32 is the alt_obs_dtype side line')
@@ -604,14 +612,18 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             visible = len(os.sched_getaffinity(0))
-            workers = args.cpu_workers or min(BOX_CPU_SHARE, visible)
+            quota = cgroup_cpus()
+            usable = min(visible, quota) if quota else visible
+            workers = args.cpu_workers or usable
             v, n, wall = cpu_baseline(args.config, args.cpu_seconds, workers, 12345)
             cpu = {"value": round(v, 1), "unit": "env-steps/s", "cores": workers, "kind": "port",
                    "per_core": round(v / workers, 1),
+                   "cores_how": f"usable cores = min(affinity {visible}, cgroup cpu.max quota "
+                                f"{quota if quota else 'none'}); worker sweep 1..128 on the GPU box saturates at the "
+                                f"16-CPU quota (profiles/r04_cpu_sweep.json)",
                    "sample": f"{n} env-steps of {args.config} (obs incl., auto-reset) on {workers} processes x "
                              f"{wall:.1f}s, C restatement oracle/mfg_oracle.c, 1 env per process (independent "
-                             f"envs: linear in cores); {visible} cores visible, the box allots {BOX_CPU_SHARE} "
-                             f"per GPU; {cpu_model()}"}
+                             f"envs: linear in cores up to the quota); {cpu_model()}"}
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "n_ranks_rccl": n_ranks,
