@@ -409,6 +409,9 @@ static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice")
 #ifndef MFG_RP_BR
 #define MFG_RP_BR 0
 #endif
+#ifndef MFG_RP_FT
+#define MFG_RP_FT 0
+#endif
 #ifndef RP_SERIAL_FWD
 #define RP_SERIAL_FWD 4  // blocks with at most this many forwards resolve them serially (no LDS table)
 #endif
@@ -559,8 +562,35 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     if (popc(cm) > RP_SERIAL_FWD) cm = 0;
 #endif
     if (cm) {
+#if MFG_RP_FT
+      // (variant) tags (ctr mod 2^16) << 16 for both table uses below, so entries of either kind order correctly
+      ctr++;
+      if (__builtin_expect((ctr & 0xFFFFu) == 0u, 0)) {  // tag wrap: clear the rank table, skip tag 0
+        ptab[lane] = 0u;
+        wave_sync();
+        ctr++;
+      }
+      const uint32_t tg16 = ctr & 0xFFFFu;
+#endif
       if (popc(cm) <= RP_SERIAL_FWD) {
         const int keyv = icur - j;  // the rank whose i equals this lane's j
+#if MFG_RP_FT
+        // one pass through the rank table: every source s writes tag | V_s at rank icur - j_s by an atomic exchange
+        // (conflicting lanes apply in lane order: the last source wins, as in the walk below); each lane reads its
+        // own rank. Exact unless a source is itself a target (a chain): then the serial walk on the original values
+        {
+          const bool fwd = lanes(cm);
+          if (fwd) atomicExch(&ptab[keyv], (tg16 << 16) | (uint32_t)v);
+          wave_sync();
+          const uint32_t te = ptab[A & 63];
+          const bool hit = (te >> 16) == tg16;
+          if (__builtin_expect((ballot(hit) & cm) == 0, 1)) {
+            v = hit ? (int)(te & 0xFFFFu) : v;
+            cm = 0;
+          }
+        }
+        if (cm)
+#endif
         do {
           const int s = ffs64(cm);
           asm volatile("s_bitset0_b64 %0, %1" : "+s"(cm) : "s"(s));
@@ -570,12 +600,20 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
         } while (cm);
       } else {
         const bool fwd = lanes(cm);
+#if MFG_RP_FT
+        const uint32_t tag = tg16 << 16;
+        atomicMax(&ptab[fwd ? icur - j : lane], fwd ? tag | (uint32_t)lane : 0u);  // max with 0: no-op
+        wave_sync();
+        const uint32_t tp = ptab[A & 63];
+        int ptr = (acc && (tp >> 16) == tg16) ? (int)(tp & 63u) : -1;
+#else
         ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
         const uint32_t tag = ctr << 6;
         atomicMax(&ptab[fwd ? icur - j : lane], fwd ? tag | (uint32_t)lane : 0u);  // max with 0: no-op
         wave_sync();
         const uint32_t tp = ptab[A & 63];
         int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
+#endif
         while (ballot(ptr >= 0)) {
           const int src = ptr >= 0 ? ptr : lane;
           const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
