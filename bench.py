@@ -489,12 +489,15 @@ def main():
         # the same stream, hipBLASLt), i.e. the policy input from materialised obs
         emb_d = torch.empty((F * B * A, args.emb), device=dev)
         wt = w.t().contiguous()
+        # dense f32 obs (the policy's input precision) whatever the headline's obs dtype
+        obs32 = obs if obs.dtype == torch.float32 else torch.zeros((F,) + eng.obs_shape(), dtype=torch.float32,
+                                                                   device=dev)
 
         def proj(k):
-            torch.matmul(obs[:k].reshape(k * B * A, -1), wt, out=emb_d[:k * B * A])
-        el4 = timed(packed_steps, None, after=proj)
+            torch.matmul(obs32[:k].reshape(k * B * A, -1), wt, out=emb_d[:k * B * A])
+        el4 = timed(packed_steps, obs32, after=proj)
         dv = B * world * packed_steps / el4
-        del emb_d
+        del emb_d, obs32
         packed = {"obs": f"packed entries (cap {args.cap}: u16 index + f32 value per nonzero, i32 count)",
                   "value": round(ev, 1), "unit": "env-steps/s", "steps": packed_steps,
                   "ms_per_step": round(el5 / packed_steps * 1e3, 4), "algo_bytes_per_env_step": pe_bytes,
