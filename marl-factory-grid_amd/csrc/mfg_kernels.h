@@ -2951,7 +2951,14 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
 #ifndef MFG_OBS_NT64
 #define MFG_OBS_NT64 1
 #endif
-        if (sizeof(OT) == 8 && !MFG_OBS_NT64) {  // f64 rows (392 B at C3): plain stores, merged into whole lines in L2
+#ifndef MFG_OBS_PLAIN_ROW
+#define MFG_OBS_PLAIN_ROW 1024
+#endif
+        // multi-wave render with short layer rows (< MFG_OBS_PLAIN_ROW bytes: C4's 9 x 9 windows): plain stores,
+        // which merge a row's partial lines with the next layer's in L2 before they go to HBM (C4 k_obs f64
+        // 2.63 -> 1.78 ms, f32 1.87 -> 1.39). Long rows (C5's 17 x 17: 79.8 -> 87.6 ms) and the single-wave render
+        // (C3: the next k_logic's records stay in L2, 0.132 vs 0.146 ms) keep non-temporal stores.
+        if ((sizeof(OT) == 8 && !MFG_OBS_NT64) || (MW && dd * (int)sizeof(OT) < MFG_OBS_PLAIN_ROW)) {
           if (inwin) *op = out;
         } else {
           if (inwin) __builtin_nontemporal_store(out, op);
