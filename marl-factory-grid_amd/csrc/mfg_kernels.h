@@ -2951,14 +2951,16 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
 #ifndef MFG_OBS_NT64
 #define MFG_OBS_NT64 1
 #endif
-#ifndef MFG_OBS_PLAIN_ROW
-#define MFG_OBS_PLAIN_ROW 1024
+#ifndef MFG_OBS_PLAIN_PTS
+#define MFG_OBS_PLAIN_PTS 12
 #endif
-        // multi-wave render with short layer rows (< MFG_OBS_PLAIN_ROW bytes: C4's 9 x 9 windows): plain stores,
-        // which merge a row's partial lines with the next layer's in L2 before they go to HBM (C4 k_obs f64
-        // 2.63 -> 1.78 ms, f32 1.87 -> 1.39). Long rows (C5's 17 x 17: 79.8 -> 87.6 ms) and the single-wave render
-        // (C3: the next k_logic's records stay in L2, 0.132 vs 0.146 ms) keep non-temporal stores.
-        if ((sizeof(OT) == 8 && !MFG_OBS_NT64) || (MW && dd * (int)sizeof(OT) < MFG_OBS_PLAIN_ROW)) {
+        // multi-wave render with short rays (<= MFG_OBS_PLAIN_PTS points: windows up to 11 x 11, C4's 9 x 9 rows of
+        // 648 B in f64): plain stores, which merge a row's partial lines with the next layer's in L2 before they go
+        // to HBM (C4 k_obs f64 2.63 -> 1.78 ms, f32 1.87 -> 1.39). Longer rows (C5's 17 x 17: 79.8 -> 87.6 ms plain)
+        // and the single-wave render (C3: the next k_logic's records stay in L2, 0.132 vs 0.146 ms) keep
+        // non-temporal stores. Compile-time: a run-time choice between the two stores gets merged into one store
+        // without the non-temporal hint.
+        if constexpr ((sizeof(OT) == 8 && !MFG_OBS_NT64) || (MW && MAXPTS <= MFG_OBS_PLAIN_PTS)) {
           if (inwin) *op = out;
         } else {
           if (inwin) __builtin_nontemporal_store(out, op);
