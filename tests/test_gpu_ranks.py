@@ -94,3 +94,21 @@ def test_bench_launcher_two_ranks_share_gpu(tmp_path):
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
     assert line['n_gpus'] == 2 and line['n_ranks_rccl'] == 2 and 'launcher' in line
     assert line['config']['global_batch'] == 2 * 4096 and line['value'] > 0
+
+
+def test_bench_default_lines_run(tmp_path):
+    """bench.py with its default lines (f64 headline, the other obs dtype, packed entries, fused projection,
+    dense f32 + projection GEMM, CPU baseline) on a small batch: the run the driver makes, shortened. Every side
+    line must be present and positive (a dtype mismatch in one of them once crashed the default run)."""
+    if not gpu_available():
+        pytest.skip('no GPU')
+    r = subprocess.run([sys.executable, str(ROOT / 'bench.py'), '--batch', '4096', '--warmup', '16', '--steps', '32',
+                        '--cpu-seconds', '1'], capture_output=True, text=True, timeout=500)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
+    assert line['value'] > 0 and 'f64 obs' in line['dtype']
+    assert line['alt_obs_dtype']['value'] > 0 and line['alt_obs_dtype']['obs'] == 'f32'
+    p = line['packed_obs']
+    assert p['value'] > 0 and p['fused_proj']['value'] > 0 and p['dense_f32_plus_proj']['value'] > 0
+    assert line['cpu_baseline']['value'] > 0 and line['cpu_baseline']['cores'] >= 1
+    assert line['roofline']['frac_sec8d'] > 0 and line['parity']['timed_mode_test']
