@@ -691,10 +691,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     e->overlap = MFG_RESET_OVERLAP == 2 || (MFG_RESET_OVERLAP == 1 && (long long)h.A * h.nf >= 16384);
     // with long resets (overlap) and a rule that consumes the floor order inside a step, the envs that finish
     // or respawn dirt would otherwise pay up to K steps of debt on the critical path (C4: 6.7 -> 7.4M env-steps/s)
-#ifndef MFG_REPLAY_EACH
-#define MFG_REPLAY_EACH 1  // A/B switch: 0 = one replay per call on every spec (k_replay_sel before each step)
-#endif
-    e->replay_each = MFG_REPLAY_EACH && e->overlap && h.step_rng;
+    e->replay_each = e->overlap && h.step_rng;
     // render shape: one wave per env, or (ray length >= 10) one env per workgroup of nwv waves sharing the cell
     // map, whichever keeps more waves per CU (C5: 3 single-wave slices of 49 KB fit a CU, 2 workgroups of 4)
     {

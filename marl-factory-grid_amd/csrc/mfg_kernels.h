@@ -403,24 +403,12 @@ __device__ __forceinline__ uint32_t lds_xchg_u16_wait(uint32_t old, uint16_t* p)
 #define RP_STAB_N 65
 #define RP_HDR_N 8  // header ints k_replay keeps in its slice (H_DEBT, H_MT_IDX)
 static_assert(H_DEBT < RP_HDR_N && H_MT_IDX < RP_HDR_N, "k_replay header slice");
-#ifndef MFG_RP_BAND
-#define MFG_RP_BAND 0
-#endif
-#ifndef MFG_RP_BR
-#define MFG_RP_BR 0
-#endif
-#ifndef MFG_RP_FT
-#define MFG_RP_FT 0
-#endif
 #ifndef RP_SERIAL_FWD
 #define RP_SERIAL_FWD 4  // blocks with at most this many forwards resolve them serially (no LDS table)
 #endif
 // The chunk's acceptance fixed point: from the seed m, iterate m = ballot(mbcnt(m) <= c) until it is stable;
 // returns A = mbcnt(m) (#accepted lanes below this one) and leaves the accepted set in m.
 __device__ __forceinline__ int accept_ranks(u64& m, int c) {
-#if MFG_RP_BR & 1  // two rounds before the first stability test (92% of chunks need two): one loop branch less per chunk
-  m = ballot(mbcnt(m) <= c);
-#endif
   for (;;) {
     const int A = mbcnt(m);
     const u64 m2 = ballot(A <= c);
@@ -438,21 +426,9 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   uint32_t* mt = e.mt();
   const int lane = e.lane;
   int first_j = -1;
-#ifndef MFG_RP_SINK
-#define MFG_RP_SINK 1
-#endif
-#ifndef MFG_RP_YWC
-#define MFG_RP_YWC 0
-#endif
-#ifndef MFG_RP_IW
-#define MFG_RP_IW 0
-#endif
-#if MFG_RP_SINK  // 128 B: one u16 per lane; lanes l and l + 32 share a dword: they sit in different lane groups of
-                 // the exchange, so the rejected lanes' sink edits of one group never hit the same dword
+  // 128 B: one u16 per lane; lanes l and l + 32 share a dword: they sit in different lane groups of the exchange,
+  // so the rejected lanes' sink edits of one group never hit the same dword
   uint16_t* sink = (uint16_t*)e.scratch + (((lane & 31) << 1) | (lane >> 5));
-#else
-  uint16_t* sink = (uint16_t*)e.scratch + lane;  // 128 B: one u16 per lane
-#endif
   uint32_t* ptab = e.stab;
   const int lo = 1;
   int idx = e.H(H_MT_IDX);
@@ -466,13 +442,6 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   // words are already in yw follows from idx alone (a twisted state had idx >= 624 > 560).
   uint32_t yw = idx <= 560 ? mt[idx + lane] : 0u;
   const int lane34 = (3 * lane) >> 2;
-#if MFG_RP_BAND
-  // the width band kept across chunks: sh = 32 - k (k = bitlen(icur + 1)) and its lowest i, blo = max(lo, 2^(k-1) - 1);
-  // both change only where a chunk fills its band (nacc = span + 1, i.e. inext < blo), which is also the only case
-  // where fewer than 64 words are consumed: one scalar test per chunk instead of the width and consumed arithmetic
-  int sh = __clz(icur + 1);
-  int blo = max(lo, (int)(0x80000000u >> sh) - 1);
-#endif
   while (icur >= lo) {
     if (idx > 560) {
       if (idx >= 624) {
@@ -490,21 +459,14 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
         yw = jw < 624 ? mt[jw < 624 ? jw : 0] : nw;
       }
     }
-#if MFG_RP_BR & 2  // the chunks between two refills: one exit test per chunk (the shuffle's end or the state's refill)
-    for (;;) {
-#endif
     const uint32_t y = TOP14 ? mt_temper3(yw) : mt_temper(yw);
     // One bit width per chunk: k = bitlen(icur + 1), and the chunk stops where bitlen(i + 1) would
     // change (i < 2^(k-1) - 1) or at lo. Within it accept <=> A <= c = min(icur - r, span), with
     // r = y >> (32 - k) fixed per lane, and lanes whose A exceeds span are not consumed (their words
     // start the next chunk). So every chunk takes the same branch-free path, power-of-two crossings
     // and the i < 64 tail included.
-#if MFG_RP_BAND
-    const int span = icur - blo;  // highest rank at width k
-#else
     const int sh = __clz(icur + 1);
     const int span = icur - max(lo, (int)(0x80000000u >> sh) - 1);  // highest rank at width k
-#endif
     uint32_t r = y >> sh;
     const int c = min(icur - (int)r, span);
     // A_l = #accepted lanes < l: Jacobi iteration from a seed at A_l ~ 3l/4 (the mean acceptance; 1.91 rounds per
@@ -519,20 +481,8 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     const int nacc = popc(m);
     // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1), and then
     // exactly the lanes up to the last accepted one (scalar, no vector compare)
-#if MFG_RP_BAND
-    const int inext = icur - nacc;
-    int consumed = 64;
-    if (__builtin_expect(inext < blo, 0)) {  // the band filled: the chunk ends it; the next chunk starts the next band
-      asm volatile("; band end" ::);  // a real branch: the compiler would otherwise compute the rare path every chunk
-      consumed = 64 - __builtin_clzll(m);
-      sh = __clz(inext + 1);
-      blo = max(lo, (int)(0x80000000u >> sh) - 1);
-    }
-    const int idxn = idx + consumed;
-#else
     const int consumed = nacc > span ? 64 - __builtin_clzll(m) : 64;
     const int inext = icur - nacc, idxn = idx + consumed;
-#endif
 #ifndef MFG_ABLATE_NOSWAP
     if constexpr (!SWAP) {
       if (first_j < 0 && m) first_j = rl((int)r, ffs64(m));
@@ -562,35 +512,8 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     if (popc(cm) > RP_SERIAL_FWD) cm = 0;
 #endif
     if (cm) {
-#if MFG_RP_FT
-      // (variant) tags (ctr mod 2^16) << 16 for both table uses below, so entries of either kind order correctly
-      ctr++;
-      if (__builtin_expect((ctr & 0xFFFFu) == 0u, 0)) {  // tag wrap: clear the rank table, skip tag 0
-        ptab[lane] = 0u;
-        wave_sync();
-        ctr++;
-      }
-      const uint32_t tg16 = ctr & 0xFFFFu;
-#endif
       if (popc(cm) <= RP_SERIAL_FWD) {
         const int keyv = icur - j;  // the rank whose i equals this lane's j
-#if MFG_RP_FT
-        // one pass through the rank table: every source s writes tag | V_s at rank icur - j_s by an atomic exchange
-        // (conflicting lanes apply in lane order: the last source wins, as in the walk below); each lane reads its
-        // own rank. Exact unless a source is itself a target (a chain): then the serial walk on the original values
-        {
-          const bool fwd = lanes(cm);
-          if (fwd) atomicExch(&ptab[keyv], (tg16 << 16) | (uint32_t)v);
-          wave_sync();
-          const uint32_t te = ptab[A & 63];
-          const bool hit = (te >> 16) == tg16;
-          if (__builtin_expect((ballot(hit) & cm) == 0, 1)) {
-            v = hit ? (int)(te & 0xFFFFu) : v;
-            cm = 0;
-          }
-        }
-        if (cm)
-#endif
         do {
           const int s = ffs64(cm);
           asm volatile("s_bitset0_b64 %0, %1" : "+s"(cm) : "s"(s));
@@ -600,20 +523,12 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
         } while (cm);
       } else {
         const bool fwd = lanes(cm);
-#if MFG_RP_FT
-        const uint32_t tag = tg16 << 16;
-        atomicMax(&ptab[fwd ? icur - j : lane], fwd ? tag | (uint32_t)lane : 0u);  // max with 0: no-op
-        wave_sync();
-        const uint32_t tp = ptab[A & 63];
-        int ptr = (acc && (tp >> 16) == tg16) ? (int)(tp & 63u) : -1;
-#else
         ctr++;  // tables are zeroed at kernel start; < 2^26 chunks per launch
         const uint32_t tag = ctr << 6;
         atomicMax(&ptab[fwd ? icur - j : lane], fwd ? tag | (uint32_t)lane : 0u);  // max with 0: no-op
         wave_sync();
         const uint32_t tp = ptab[A & 63];
         int ptr = (acc && (tp >> 6) == ctr) ? (int)(tp & 63u) : -1;
-#endif
         while (ballot(ptr >= 0)) {
           const int src = ptr >= 0 ? ptr : lane;
           const int v2 = __shfl(v, src), p2 = __shfl(ptr, src);
@@ -631,19 +546,11 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
       const uint32_t ad = (uint32_t)(uintptr_t)(acc ? &perm[j] : sink) & ~3u;
       asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(F) : "v"(ad), "v"(0xFFFFu << (sh & 31u)),
                    "v"((uint32_t)v << (sh & 31u)) : "memory");
-#if MFG_RP_YWC || (MFG_RP_BR & 2)  // the next chunk's words loaded unconditionally from min(idxn, 560) (reloaded at the top if idxn > 560)
-      yw = mt[min(idxn, 560) + lane];
-#else
       if (idxn <= 560) yw = mt[idxn + lane];
-#endif
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(F) : : "memory");
       asm("v_lshrrev_b32 %0, %1, %2" : "=v"(F) : "v"(sh), "v"(F));  // low 5 bits of sh; the i write keeps 16 bits
     }
-#if MFG_RP_IW  // rejected lanes write their sink instead of an exec-masked write
-    *(acc ? pi : sink) = (uint16_t)F;
-#else
     if (acc) *pi = (uint16_t)F;
-#endif
     wave_sync();
     }
 #else
@@ -651,10 +558,6 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
 #endif
     icur = inext;
     idx = idxn;
-#if MFG_RP_BR & 2
-    if (__builtin_expect(((icur - lo) | (560 - idx)) < 0, 0)) break;  // icur < lo or idx > 560: one sign test
-    }
-#endif
   }
   if (idx > 624) {  // words of the next state were consumed: make the state canonical (CPython's mti)
     mt_twist(e);
@@ -2948,9 +2851,6 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
 #if defined(MFG_ABLATE_OB_NOSTORE)  // timing only: the values are computed, (almost) never stored
         if (inwin && out == (OT)-12345.0) *op = out;
 #else
-#ifndef MFG_OBS_NT64
-#define MFG_OBS_NT64 1
-#endif
 #ifndef MFG_OBS_PLAIN_PTS
 #define MFG_OBS_PLAIN_PTS 12
 #endif
@@ -2960,7 +2860,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         // and the single-wave render (C3: the next k_logic's records stay in L2, 0.132 vs 0.146 ms) keep
         // non-temporal stores. Compile-time: a run-time choice between the two stores gets merged into one store
         // without the non-temporal hint.
-        if constexpr ((sizeof(OT) == 8 && !MFG_OBS_NT64) || (MW && MAXPTS <= MFG_OBS_PLAIN_PTS)) {
+        if constexpr (MW && MAXPTS <= MFG_OBS_PLAIN_PTS) {
           if (inwin) *op = out;
         } else {
           if (inwin) __builtin_nontemporal_store(out, op);
