@@ -940,7 +940,18 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     {
     PROF_BEGIN(e, st);
     if (e->h.bfs_bytes) {
-    hipLaunchKernelGGL((k_logic<true, true>), GEOMW(e->h.lds_logic, logic_wpb), st,
+    // maintainers: the envs where no maintainer re-routes (and no dirt spawn fires) this step run with the step
+    // prefix + maintainer state/paths staged (no MT, permutation or BFS scratch: several times the occupancy), the
+    // rest with the full record
+    const int ms0 = e->h.L.o_mstate & ~15;
+    const int lm_lds = e->h.L.o_logic + (((e->h.L.o_grank + 15) & ~15) - ms0) + 4 * MFG_WAVE;
+    hipLaunchKernelGGL((k_logic<true, true, 1>), GEOMW(lm_lds, logic_wpb), st,
+                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
+                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
+                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
+                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
+                       auto_reset, e->rd_slot);
+    hipLaunchKernelGGL((k_logic<true, true, 2>), GEOMW(e->h.lds_logic, logic_wpb), st,
                        e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
                        env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
                        done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,

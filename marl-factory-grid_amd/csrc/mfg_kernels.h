@@ -88,6 +88,7 @@ struct Env {
   uint8_t* bfs;     // maintainer BFS scratch (full-record kernels of specs with MoveMaintainers)
   int* hdrp;        // header slots (inside the record image, or a separate slice in k_replay)
   int lane;
+  int mdelta = 0;   // where the maintainer state/paths sit relative to their record offset (k_logic<.., SEL 1>)
   __device__ int* hdr() const { return hdrp; }
   __device__ int* rctr() const { return (int*)(lds + S->L.o_rule_ctr); }
   __device__ int* agpos() const { return (int*)(lds + S->L.o_agent_pos); }
@@ -110,8 +111,8 @@ struct Env {
   __device__ uint16_t* perm() const { return (uint16_t*)(lds + S->L.o_perm); }
   __device__ int* machines() const { return (int*)(lds + S->L.o_machines); }
   __device__ int* maints() const { return (int*)(lds + S->L.o_maints); }
-  __device__ int* mst(int k) const { return (int*)(lds + S->L.o_mstate) + k * S->mstate_ints; }
-  __device__ uint16_t* mpath(int k) const { return (uint16_t*)(lds + S->L.o_mpath) + k * S->path_cap; }
+  __device__ int* mst(int k) const { return (int*)(lds + S->L.o_mstate + mdelta) + k * S->mstate_ints; }
+  __device__ uint16_t* mpath(int k) const { return (uint16_t*)(lds + S->L.o_mpath + mdelta) + k * S->path_cap; }
   __device__ uint16_t* grank() const { return (uint16_t*)(lds + S->L.o_grank); }
   // uniform header access
   __device__ int H(int k) const { return uni(hdr()[k]); }
@@ -3074,9 +3075,19 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   // (clean_up/rules.py:49-59). The first launch has already stepped (and counted down) the other envs when the
   // second runs, so it marks the envs it leaves in rd_flag (2), which the second takes and overwrites.
   if constexpr (SEL == 1) {
-    const int* rc = (const int*)(state + (size_t)env * S->L.size + S->L.o_rule_ctr);
+    const uint8_t* grec = state + (size_t)env * S->L.size;
+    const int* rc = (const int*)(grec + S->L.o_rule_ctr);
     bool fire = false;
     for (uint32_t m = S->respawn_mask; m; m &= m - 1) fire |= uni(rc[__ffs(m) - 1]) == 0;
+    if constexpr (MAINT) {
+      // a maintainer needs the floor order / MT / BFS only when its path is used up at its tick (maint_tick:
+      // a new route, maintenance/entitites.py get_move_action); nothing changes its path before that tick
+      const int nk = uni(((const int*)(grec + S->L.o_hdr))[H_N_MAINTS]);
+      for (int k = 0; k < nk; k++) {
+        const int* st = (const int*)(grec + S->L.o_mstate) + k * S->mstate_ints;
+        fire |= uni(st[MS_PATH_HEAD]) >= uni(st[MS_PATH_N]);
+      }
+    }
     if (fire) {
       if (lane_id() == 0) S->rd_flag[env] = 2;
       return;
@@ -3085,13 +3096,18 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     if (uni((int)S->rd_flag[env]) != 2) return;
   }
   Env e;
-  uint8_t* slice = smem + (size_t)wid * S->lds_logic;
-  constexpr bool full = FULL;
+  // MAINT, SEL 1: the step prefix, then the maintainer state and paths [o_mstate, o_grank) (16-B rounded) right
+  // after it instead of at their record offset (mdelta), then the count scratch: no MT, permutation or BFS scratch
+  constexpr bool lm = MAINT && SEL == 1;
+  const int ms0 = S->L.o_mstate & ~15, mlen = lm ? ((S->L.o_grank + 15) & ~15) - ms0 : 0;
+  uint8_t* slice = smem + (size_t)wid * (lm ? S->L.o_logic + mlen + 4 * MFG_WAVE : S->lds_logic);
+  constexpr bool full = FULL && !lm;
   if (full) {
     env_full(S, slice, e, env);
   } else {
-    e.S = S; e.lds = slice; e.scratch = (int*)(slice + S->L.o_logic); e.stab = nullptr; e.cmap = nullptr;
-    e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
+    e.S = S; e.lds = slice; e.scratch = (int*)(slice + S->L.o_logic + mlen); e.stab = nullptr; e.cmap = nullptr;
+    e.bfs = nullptr; e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
+    if (lm) e.mdelta = S->L.o_logic - ms0;
   }
   uint8_t* rec = state + (size_t)env * S->L.size;
   // FULL without maintainers: a RespawnDirt rule is the only in-step reader of the MT state and the floor order, and
@@ -3102,7 +3118,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   const int bytes = full && !lazy ? S->L.size : S->L.o_logic;
   // lean records of <= 1 KiB: each lane keeps its 16-B chunk and writes it back only if the step changed it
   // (most of the record is per-episode constant: frozen origins, ids, counters of idle rules)
-  const bool one_pass = (!full || lazy) && (bytes >> 4) <= MFG_WAVE;
+  const bool one_pass = (!full || lazy) && (bytes >> 4) <= MFG_WAVE;  // (lm: full is false)
   uint4 orig = make_uint4(0, 0, 0, 0);
   if (one_pass && e.lane < (bytes >> 4)) orig = ((const uint4*)rec)[e.lane];
   // the actions (a buffer load or Philox) while the record load is in flight
@@ -3122,6 +3138,10 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     rec_copy(e.lds, rec, bytes, e.lane);
   }
   wave_sync();
+  if constexpr (lm) {
+    rec_copy(e.lds + S->L.o_logic, rec + ms0, mlen, e.lane);
+    wave_sync();
+  }
   // the RNG tail [o_mt, o_mstate) rounded to 16 B (o_mt is 16-B aligned; the rounding stays inside the record)
   const int o_tail = S->L.o_mt, n_tail = (S->L.o_mstate - S->L.o_mt + 15) & ~15;
   bool rng_tail = false;
@@ -3155,6 +3175,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     rec_copy(rec, e.lds, bytes, e.lane);
   }
   if (lazy && rng_tail) rec_copy(rec + o_tail, e.lds + o_tail, n_tail, e.lane);
+  if constexpr (lm) rec_copy(rec + ms0, e.lds + S->L.o_logic, mlen, e.lane);
 }
 #endif
 
