@@ -987,7 +987,6 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     }
     const int rd_cur = e->rd_slot;
     e->rd_slot ^= 1;  // the next k_logic appends to the other list (and empties this one after k_resetdone)
-    if (e->replay_each && k + 1 < K && replay_impl(e, stream)) return -1;
     void* obs_k = obs && obs_dtype != MFG_OBS_PACKED ? (void*)((uint8_t*)obs + (size_t)k * obs_row) : obs;
 #ifdef MFG_ABLATE_NOOBS
     obs_k = nullptr;
@@ -996,6 +995,11 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     // caller's stream renders every other env (k_logic's rd_flag tells k_obs which to leave out): a step's
     // resets are a few hundred latency-bound waves (C4: ~2.4 ms) that the full render hides.
     const bool split = e->overlap && auto_reset && obs_k;
+    // the per-step replay (replay_each): on the second stream after the resets, beside the render when split (the
+    // render reads the step prefix and cell map, the replay writes MT / permutation and two header words the
+    // render does not read; the next step's k_logic waits for both streams)
+    const bool replay_now = e->replay_each && k + 1 < K;
+    if (replay_now && !split && replay_impl(e, stream)) return -1;
     hipStream_t rs = split ? e->aux : st;
     if (split) {
       HIPCHK(hipEventRecord(e->ev_fork, st));
@@ -1017,6 +1021,7 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     if (split) {
       const int32_t* lst = e->h.rd_list + (size_t)rd_cur * (size_t)(e->B + 2);
       if (launch_obs(e, obs_k, obs_dtype, rs, k, nullptr, lst, MFG_K_OBS_DONE)) return -1;
+      if (replay_now && replay_impl(e, rs)) return -1;
     }
     if (split) {
       if (launch_obs(e, obs_k, obs_dtype, st, k, e->h.rd_flag, nullptr, MFG_K_OBS)) return -1;
