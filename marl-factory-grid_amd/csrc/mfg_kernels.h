@@ -2977,8 +2977,8 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
 // SGPR spill (C3: 0.1505 -> 0.1303 ms per launch). The same request on the dense k_obs spills ~90 SGPRs into VGPR
 // lanes and made it slower (0.433 -> 0.451 ms), so k_obs keeps 7.
 #define MFG_WPE_LOGIC(n) __attribute__((amdgpu_waves_per_eu(n)))
-// the single-wave render (short rays) asks for 7 waves per SIMD with f32 obs and 8 with f64 (C3 A/B, round 4: f64
-// k_obs 0.4995 -> 0.495 ms at 8 despite 84 SGPRs spilled into VGPR lanes; f32 0.399 -> 0.466 ms at 8)
+// the single-wave render (short rays) asks for 7 waves per SIMD. 8 (round 4 A/B): C3 f64 k_obs 0.4995 -> 0.495 ms,
+// but C3 f32 0.399 -> 0.466 and C2 f64 0.032 -> 0.038 ms (84 SGPRs spilled into VGPR lanes, 2 VGPRs to scratch)
 
 // full-record slice: [record][scratch][shuffle tables][BFS scratch if it fits]
 __device__ __forceinline__ void env_full(SpecP S, uint8_t* slice, Env& e, long long env) {
@@ -3252,7 +3252,7 @@ __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* 
 // on the engine's second stream; null = none). With auto-reset, mfg_step renders the envs that did not finish
 // on the caller's stream while the finished ones are reset and rendered beside it.
 template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT>
-static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 ? (sizeof(OT) == 8 ? 8 : 7) : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
+static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(MAXPTS <= 8 ? 7 : 1))) k_obs(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                       OT* obs, ObsPacked pk, const uint8_t* skip) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
