@@ -23,7 +23,9 @@ bounded sample.
 Multi-GPU (weak scaling, env ranges sharded, no collective in the data path): either the driver's
 `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`, or plain `python bench.py --gpus N`,
 which starts the N rank processes itself (launch_ranks) before anything touches the GPU and prints rank 0's
-line. Each rank asserts that the RCCL world size equals --gpus (`n_ranks_rccl` in the line).
+line. Under a launcher (WORLD_SIZE set, N = 1 included) every rank joins one process group (nccl = RCCL) whose size
+must equal --gpus; the line reports `backend` and `n_ranks_rccl` (nccl groups only; gloo lines say `n_ranks_gloo`),
+and the barrier, the MAX all-reduce of the elapsed time and the metrics all-reduce run on that group.
 """
 import argparse
 import json
@@ -154,25 +156,31 @@ def cpu_model():
 
 
 def stream_copy_gbs(dev, nbytes=2 << 30, reps=10):
-    """Measured HBM stream-copy bandwidth on this GPU: a device-to-device copy of `nbytes`
-    moves 2 x nbytes; best of `reps` after a warm-up, timed with events on the current stream."""
+    """Measured HBM stream-copy bandwidth on this GPU: the library's hand-written 16-B-per-lane copy
+    kernel (mfg_hbm_copy) over `nbytes` moves 2 x nbytes; best of `reps` after a warm-up, timed with events on the
+    stream the kernel is launched on. torch's copy_ is reported beside it (it measured ~4.5 TB/s in round 4)."""
     import torch
+    from mfg_amd.engine import hbm_copy
     a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
     a.fill_(1.0)
-    b.copy_(a)
-    best = None
-    for _ in range(reps):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        b.copy_(a)
-        e.record()
-        e.synchronize()
-        t = s.elapsed_time(e) * 1e-3
-        best = t if best is None else min(best, t)
+    stream = torch.cuda.current_stream(dev)
+    res = {}
+    for name, fn in (('hip_copy16', lambda: hbm_copy(b, a, stream)), ('torch_copy_', lambda: b.copy_(a))):
+        fn()
+        best = None
+        for _ in range(reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            fn()
+            e.record(stream)
+            e.synchronize()
+            t = s.elapsed_time(e) * 1e-3
+            best = t if best is None else min(best, t)
+        res[name] = round(2 * nbytes / best / 1e9, 1)
     del a, b
     torch.cuda.empty_cache()
-    return 2 * nbytes / best / 1e9
+    return res
 
 
 def load_pmc(workload):
@@ -258,15 +266,18 @@ def launch_ranks(n, argv, share_gpu=False, dry_run=False, rank_timeout=900.0):
 
 
 def init_ranks(args):
-    """(world, rank, local) of this process; joins the process group for world > 1 and checks that the
-    collective backend's world size equals --gpus."""
+    """(world, rank, local, n_ranks, backend) of this process. Under a launcher (WORLD_SIZE set, e.g. the driver's
+    `torch.distributed.run --nproc-per-node N`, N = 1 included) every rank joins one process group (nccl = RCCL unless
+    --backend says otherwise) and checks that its world size equals --gpus; a bare single-process run has no group
+    (backend None)."""
+    launched = 'WORLD_SIZE' in os.environ
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if args.gpus > 1 and world != args.gpus:
+    if (args.gpus > 1 or launched) and world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    if world == 1:
-        return world, rank, local, 1
+    if not launched:
+        return world, rank, local, 1, None
     import torch
     import torch.distributed as dist
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
@@ -281,12 +292,25 @@ def init_ranks(args):
         else:
             dist.init_process_group(args.backend)
     n_ranks = dist.get_world_size()
-    if n_ranks != world or (args.gpus > 1 and n_ranks != args.gpus):
+    if n_ranks != world or n_ranks != args.gpus:
         raise SystemExit(f"bench.py: process group has {n_ranks} ranks, expected {world} (--gpus {args.gpus})")
-    return world, rank, local, n_ranks
+    return world, rank, local, n_ranks, dist.get_backend()
 
 
-def dry_run(args, world, rank, n_ranks):
+def rank_fields(n_ranks, backend):
+    """How the line's ranks were joined: n_ranks_rccl only for an nccl (= RCCL on ROCm) group."""
+    f = {"backend": backend}
+    if backend == 'nccl':
+        f["n_ranks_rccl"] = n_ranks
+    elif backend is not None:
+        f[f"n_ranks_{backend}"] = n_ranks
+    else:
+        f["n_ranks_rccl"] = None
+        f["process_group"] = "none (single process, not started by a launcher)"
+    return f
+
+
+def dry_run(args, world, rank, n_ranks, backend):
     """CPU rehearsal of the multi-rank protocol (no GPU, gloo): env ranges, barrier-bracketed timed region,
     MAX over ranks and the metrics all-reduce, with the same output fields as the GPU line."""
     import torch
@@ -294,29 +318,29 @@ def dry_run(args, world, rank, n_ranks):
     from mfg_amd.shard import env_range, allreduce_metrics
     B = args.batch
     first, count = env_range(rank, world, B)
-    if world > 1:
+    if backend:
         dist.barrier()
     t0 = time.perf_counter()
     acc = 0
     for _ in range(args.steps):
         acc += count
     elapsed = time.perf_counter() - t0 + 1e-3 * (rank + 1)
-    if world > 1:
+    if backend:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     m = allreduce_metrics(torch.tensor([float(acc)], dtype=torch.float64))
     ranges = [None] * world
-    if world > 1:
+    if backend:
         dist.all_gather_object(ranges, (first, count))
     else:
         ranges = [(first, count)]
     if rank == 0:
         print(json.dumps({"metric": METRIC, "dry_run": True, "value": B * world * args.steps / elapsed,
-                          "n_gpus": world, "n_ranks_rccl": n_ranks, "steps": args.steps, "max_elapsed_s": elapsed,
+                          "n_gpus": world, **rank_fields(n_ranks, backend), "steps": args.steps, "max_elapsed_s": elapsed,
                           "env_ranges": ranges, "metrics_allreduce": float(m[0])}), flush=True)
-    if world > 1:
+    if backend:
         dist.destroy_process_group()
 
 
@@ -352,9 +376,9 @@ def main():
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         return launch_ranks(args.gpus, sys.argv[1:], share_gpu=os.environ.get('MFG_BENCH_SHARE_GPU') == '1',
                             dry_run=args.dry_run, rank_timeout=args.rank_timeout)
-    world, rank, local, n_ranks = init_ranks(args)
+    world, rank, local, n_ranks, backend = init_ranks(args)
     if args.dry_run:
-        return dry_run(args, world, rank, n_ranks)
+        return dry_run(args, world, rank, n_ranks, backend)
 
     import torch
     import torch.distributed as dist
@@ -377,7 +401,7 @@ def main():
     eng.reset(obs=obs[0], init=True, seed_base=env_base)
     stream = torch.cuda.current_stream(dev)
     step_no = 0
-    red_dev = dev if world == 1 or args.backend == 'nccl' else torch.device('cpu')  # gloo reduces host tensors
+    red_dev = dev if backend in (None, 'nccl') else torch.device('cpu')  # gloo reduces host tensors
     episodes = torch.zeros((), dtype=torch.float64, device=red_dev)
 
     def run(n, events=None, profile=False, obs_buf=None, after=None):
@@ -406,7 +430,7 @@ def main():
 
     run(args.warmup)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if backend:
         dist.barrier()
     torch.cuda.synchronize(dev)
     calls = []
@@ -414,13 +438,13 @@ def main():
     t0 = time.perf_counter()
     run(args.steps, calls, profile=not args.no_profile)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if backend:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     prof = eng.profile_read()
     eng.profile(False)
-    if world > 1:
+    if backend:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -432,17 +456,17 @@ def main():
         """n more steps into obs_buf, timed like the headline (barrier + synchronize brackets, max over ranks)."""
         run(F, obs_buf=obs_buf, after=after)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if backend:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         run(n, obs_buf=obs_buf, after=after)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if backend:
             dist.barrier()
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t1
-        if world > 1:
+        if backend:
             t = torch.tensor([el], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -591,27 +615,17 @@ def main():
                     "unit": "GB/s", "frac": round(pipe_bytes / mean_call / 1e9 / HBM_PEAK_GBS, 5),
                     "traffic": None, "kernel": "mfg_step pipeline", "mean_launch_ms": round(mean_call * 1e3, 3)}
         try:
-            peak_meas = round(stream_copy_gbs(dev), 1)
+            copies = stream_copy_gbs(dev)
         except RuntimeError:  # not enough free HBM for the 4 GiB copy pair
-            peak_meas = None
+            copies = {}
+        peak_meas = copies.get('hip_copy16')
         roof["peak_measured"] = peak_meas
-        roof["peak_measured_how"] = "device-to-device copy of 2 GiB (2 x 2 GiB moved), best of 10"
+        roof["peak_measured_how"] = ("hand-written 16-B-per-lane HIP copy kernel (mfg_hbm_copy) over 2 GiB, 2 x 2 GiB "
+                                     f"moved, best of 10; torch copy_ of the same buffers: {copies.get('torch_copy_')} GB/s")
         if peak_meas and roof.get("achieved"):
             roof["frac_of_measured"] = round(roof["achieved"] / peak_meas, 5)
-        if dom:
-            # SURVEY §8(d)'s definition charged to the dominant kernel: the whole env-step's algorithmic bytes x the
-            # env-steps one launch of it covers (k_replay: B x K), over its mean launch time. `frac` above uses the
-            # kernel's own minimal bytes (MT + permutation); this is the figure the §8(d) table reads.
-            steps_per_launch = B * (k_call if dom == 'k_replay' else 1)
-            sec8d = step_bytes * steps_per_launch / (kernels[dom]["mean_launch_ms"] * 1e-3) / 1e9
-            sec8d_f32 = ALGO_BYTES_PER_ENV_STEP * steps_per_launch / (kernels[dom]["mean_launch_ms"] * 1e-3) / 1e9 \
-                if args.config == 'large8.yaml' else None
-            roof["frac_sec8d"] = round(sec8d / HBM_PEAK_GBS, 5)
-            roof["sec8d"] = {"algo_bytes_per_env_step": step_bytes, "env_steps_per_launch": steps_per_launch,
-                             "achieved_GBs": round(sec8d, 2),
-                             "frac_with_f32_obs_bytes": round(sec8d_f32 / HBM_PEAK_GBS, 5) if sec8d_f32 else None,
-                             "how": "SURVEY §8(d) bytes per env-step (this line's obs dtype; 11,391 B with f32 obs) x "
-                                    "env-steps per launch of the dominant kernel / its mean launch time / 8 TB/s"}
+        if peak_meas and roof.get("pipeline"):
+            roof["pipeline"]["frac_of_measured"] = round(roof["pipeline"]["achieved"] / peak_meas, 5)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             visible = len(os.sched_getaffinity(0))
@@ -629,7 +643,7 @@ def main():
                              f"envs: linear in cores up to the quota); {cpu_model()}"}
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
-            "n_ranks_rccl": n_ranks,
+            **rank_fields(n_ranks, backend),
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": f"f64 rewards/battery/dirt, {args.obs_dtype} obs",
@@ -654,13 +668,16 @@ def main():
                        "side_lines": {"alt_obs_dtype": PARITY_TESTS['f32' if args.obs_dtype == 'f64' else 'f64'],
                                       "packed_obs": "tests/test_marl.py (packed rows scatter to the dense f32 obs "
                                                     "bit-exactly)"}},
+            "collectives": ({"tensors": str(red_dev), "barriers": "before and after every timed region",
+                             "max_allreduce": "elapsed time of every timed region",
+                             "metrics_allreduce_episodes": float(episodes.item())} if backend else None),
             "cpu_baseline": cpu,
             "alt_obs_dtype": alt,
             "packed_obs": packed,
         }
         print(json.dumps(out))
     eng.close()
-    if world > 1:
+    if backend:
         dist.destroy_process_group()
 
 

@@ -336,6 +336,11 @@ int mfg_profile_read(mfg_engine* e, double* total_ms, int64_t* launches, int n);
 int mfg_export_state(mfg_engine* e, void* dst, void* stream);
 int mfg_import_state(mfg_engine* e, const void* src, void* stream);
 
+/* Measurement helper (not part of the Factory.step boundary): copy nbytes (a multiple of 16, 16-B aligned device
+ * pointers) on the current device with a 16-B-per-lane streaming kernel, on `stream`. bench.py times it to report
+ * the measured HBM peak beside the 8 TB/s spec figure. */
+int mfg_hbm_copy(void* dst, const void* src, int64_t nbytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

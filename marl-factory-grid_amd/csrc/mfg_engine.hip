@@ -893,9 +893,16 @@ static int replay_impl(mfg_engine* e, void* stream) {
     hipLaunchKernelGGL(k_replay2, dim3((unsigned)e->B), dim3(2 * MFG_WAVE),
                        (size_t)e->h.lds_replay_per_wave + RP2_RING, st, e->d_spec, e->d_state, (long long)e->B,
                        (const int*)e->rp_order);
-  else
-    hipLaunchKernelGGL(k_replay, dim3((unsigned)e->B), dim3(64), (size_t)e->h.lds_replay_per_wave, st, e->d_spec,
-                       e->d_state, (long long)e->B, (const int*)e->rp_order);
+  else {
+    size_t lds = (size_t)e->h.lds_replay_per_wave;
+#ifdef MFG_RP_LDS_W
+    // measurement only (tools/gpu_r05a.sh, DESIGN §4 "k_replay, round 5"): the same kernel with its LDS slice padded so
+    // that at most MFG_RP_LDS_W waves per SIMD fit, for the occupancy curve
+    lds = std::max(lds, (size_t)((MFG_LDS_MAX / (4 * MFG_RP_LDS_W)) & ~15));
+#endif
+    hipLaunchKernelGGL(k_replay, dim3((unsigned)e->B), dim3(64), lds, st, e->d_spec, e->d_state, (long long)e->B,
+                       (const int*)e->rp_order);
+  }
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_replay launch: ") + hipGetErrorString(err));
   PROF_END(e, st, MFG_K_REPLAY);
@@ -1075,3 +1082,23 @@ static int profile_read_impl(mfg_engine* e, double* total_ms, int64_t* launches,
 
 extern "C" int64_t mfg_state_bytes(const mfg_engine* e) { return e ? (int64_t)e->h.L.size * e->B : -1; }
 extern "C" int mfg_abi_version(void) { return MFG_ABI_VERSION; }
+
+// Measured HBM peak for the bench's roofline (mfg.h mfg_hbm_copy): one 16-B non-temporal load + store per lane, one
+// lane per 16 B (tools/copy_probe.hip on the MI355X, 2 GiB: this form 6.58 TB/s of read + write bytes; plain 6.24;
+// 4-8 per lane unrolled 5.6-6.0; grid-stride loops 4.7-4.9; hipMemcpy 5.0; torch copy_ 4.5)
+typedef unsigned mfg_v4u __attribute__((ext_vector_type(4)));
+static __global__ void __launch_bounds__(256) k_hbm_copy(mfg_v4u* __restrict__ dst, const mfg_v4u* __restrict__ src,
+                                                         long long n16) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+}
+extern "C" int mfg_hbm_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if (!dst || !src || nbytes <= 0 || (nbytes & 15) || (((uintptr_t)dst | (uintptr_t)src) & 15))
+    return fail("mfg_hbm_copy: null pointer, or size/alignment not a multiple of 16 B");
+  const long long n16 = (long long)(nbytes >> 4);
+  if ((n16 + 255) / 256 > 0x7fffffffLL) return fail("mfg_hbm_copy: size too large");
+  hipLaunchKernelGGL(k_hbm_copy, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, (mfg_v4u*)dst,
+                     (const mfg_v4u*)src, n16);
+  HIPCHK(hipGetLastError());
+  return 0;
+}

@@ -3243,6 +3243,8 @@ __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* 
   } else {
     build_obs<MAXPTS, OT, MM, PK, DIRT, MW>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg, pk, wv, nwv);
   }
+  // k_obs reads only [0, o_mt) of the record and stores only this word: the replay of the same call may run beside it
+  // on the engine's second stream and writes H_DEBT / H_MT_IDX (single words) and [o_mt, o_perm + 2 nf) (replay_env)
   if ((!MW || wv == 0) && e.lane == 0 && e.hdrp[H_OVERFLOW])
     ((int*)(state + (size_t)env * S->L.size + S->L.o_hdr))[H_OVERFLOW] = 1;
   if constexpr (MW) __syncthreads();  // the shared tables are free for the workgroup's next env
@@ -3340,6 +3342,11 @@ __device__ __forceinline__ void replay_env(SpecP S, uint8_t* slice, uint8_t* rec
     uint4* dst = (uint4*)(rec + S->L.o_mt);
     for (int i = e.lane; i < n16; i += MFG_WAVE) dst[i] = src[i];
   }
+  // Word-granular header write-back, on purpose: in split mode (mfg_step, replay beside the last k_obs on the second
+  // stream) k_obs may read this record's header and store its H_OVERFLOW word at the same time. k_obs never reads
+  // H_DEBT / H_MT_IDX or anything at or past o_mt, and these two single-word stores never touch H_OVERFLOW; a vector
+  // store of the header here would race with it.
+  static_assert(H_OVERFLOW != H_DEBT && H_OVERFLOW != H_MT_IDX, "replay header words must not cover H_OVERFLOW");
   if (e.lane == 0) {
     ((int*)(rec + S->L.o_hdr))[H_DEBT] = 0;
     ((int*)(rec + S->L.o_hdr))[H_MT_IDX] = hdr[H_MT_IDX];

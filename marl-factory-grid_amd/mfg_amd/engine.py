@@ -71,6 +71,8 @@ def load_lib():
     L.mfg_profile.restype = C.c_int
     L.mfg_profile_read.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     L.mfg_profile_read.restype = C.c_int
+    L.mfg_hbm_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    L.mfg_hbm_copy.restype = C.c_int
     L.mfg_abi_version.restype = C.c_int
     if L.mfg_abi_version() != abi.ABI_VERSION:
         raise RuntimeError('libmfg_hip.so ABI version mismatch')
@@ -80,6 +82,16 @@ def load_lib():
 
 def _ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def hbm_copy(dst, src, stream=None):
+    """dst.copy_(src) through the library's 16-B-per-lane streaming kernel (mfg_hbm_copy; bench.py's measured HBM
+    peak). Both contiguous device tensors of the same byte size on the current device."""
+    import torch
+    n = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() == n and dst.is_contiguous() and src.is_contiguous()
+    st = stream if stream is not None else torch.cuda.current_stream(src.device)
+    _check(load_lib().mfg_hbm_copy(_ptr(dst), _ptr(src), n, C.c_void_p(st.cuda_stream)), 'mfg_hbm_copy')
 
 
 def _check(rc, what, h=None):

@@ -203,7 +203,7 @@ class Factory:
             try:
                 reward, done, info = fold_step(self.spec, self._host, [int(x) for x in actions], ev, pre,
                                                self.snapshot(), done)
-            except StaleStateError:
+            except BaseException:  # StaleStateError or anything custom rule code raises inside the fold
                 self._stale_step = True  # the device stepped but this step's results were never returned
                 raise
             info = dict(info)

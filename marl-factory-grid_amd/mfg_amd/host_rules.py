@@ -45,18 +45,22 @@ NO_POS = (-9999, -9999)
 # match is_move, clean_up/rules.py:79), the tick_post_step of BatteryDecharge / DoneAtBatteryDischarge (it only
 # paralyses agents, batteries/rules.py:66-87; charge changes in tick_step).
 _BATT = {'Batteries': ('charge_level', 'is_discharged')}
+_DOORS = {'Doors': ('is_open', 'is_closed', 'time_to_close')}
+_REACHED = {'Destinations': ('reached', 'was_reached')}
 _MUTATORS = {
-    'DoorAutoClose': {_info.TICK: {'Doors': ('is_open', 'is_closed', 'time_to_close')}},
-    'MoveMaintainers': {_info.TICK: {'Maintainers': None}},
+    'DoorAutoClose': {_info.TICK: _DOORS},
+    # maintainers open doors on their path through DoorUse inside their tick (maintenance/entities.py:91-100)
+    'MoveMaintainers': {_info.TICK: {'Maintainers': None, **_DOORS}},
     'BatteryDecharge': {_info.TICK: _BATT},
     'DoneAtBatteryDischarge': {_info.TICK: _BATT},
     'RespawnDirt': {_info.TICK: {'DirtPiles': None}},
-    'DestinationReachReward': {_info.TICK: {'Destinations': ('reached',)}},
-    'DoneAtDestinationReach': {_info.TICK: {'Destinations': ('reached',)}},
+    'DestinationReachReward': {_info.TICK: _REACHED},
+    'DoneAtDestinationReach': {_info.TICK: _REACHED},
     'WatchCollisions': {_info.POST: {'Agents': ('state',)}},
 }
-# rules that change state only on the steps where they emit a Result: RespawnDirt on its spawn steps
-# (clean_up/rules.py:49-59), the reach rules when a destination is reached (destinations/rules.py:33-54)
+# DoneAtDestinationReach(condition='simultaneous') also unmarks reached destinations in on_check_done when not all
+# are reached (destinations/rules.py:80-87), on any step, with or without a Result of its own
+_DONE_SIMULTANEOUS = {_info.DONE: _REACHED}
 _ON_RESULT = {'RespawnDirt', 'DestinationReachReward', 'DoneAtDestinationReach'}
 
 
@@ -74,14 +78,20 @@ def stale_state(spec, slot, phase, fired=None):
     Result this step (None = assume every rule fired); a rule in `_ON_RESULT` that did not fire changed nothing.
     The TICK view carries the agents' action results as their states, so WatchCollisions' later states do not
     leak into it."""
-    if phase in (_info.PRE, _info.DONE):
+    if phase == _info.PRE:
         return {}
+    from . import abi
     out = {}
     for i, name in enumerate(spec.rule_names):
-        if name in _ON_RESULT and fired is not None and i not in fired:
+        muts = dict(_MUTATORS.get(name, {}))
+        if name == 'DoneAtDestinationReach' and int(spec.c.rules[i].i[0]) == abi.DEST_SIMULTANEOUS:
+            muts.update(_DONE_SIMULTANEOUS)  # not filtered by `fired`: the unmarking needs no Result
+        elif name in _ON_RESULT and fired is not None and i not in fired:
             continue
-        for ph, groups in _MUTATORS.get(name, {}).items():
+        for ph, groups in muts.items():
             if ph < phase or (ph == phase and i < slot):
+                continue
+            if ph != _info.DONE and name in _ON_RESULT and fired is not None and i not in fired:
                 continue
             for g, attrs in groups.items():
                 if g == 'Agents' and ph != phase:
@@ -280,7 +290,8 @@ class StateView:
                                                                      amount=a) for i, c, a in snap.dirt])
         if 'Destinations' in spec.group_names:
             groups['Destinations'] = GroupView('Destinations', [
-                EntityView(name=f'Destination[{i}]', pos=xy(c), identifier=i, reached=bool(r)) for i, c, r in snap.dests])
+                EntityView(name=f'Destination[{i}]', pos=xy(c), identifier=i, reached=bool(r),
+                           was_reached=(lambda r=bool(r): r)) for i, c, r in snap.dests])
         if 'Batteries' in spec.group_names:
             groups['Batteries'] = GroupView('Batteries', [
                 EntityView(name=f'Battery[{a.name}]', bound_entity=a, charge_level=float(b), is_discharged=b == 0)

@@ -271,11 +271,12 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None, custom_mo
     if pomdp_r < 0:
         raise UnsupportedSpec('pomdp_r must be >= 0')
     # the ray radius is the window diameter (Q13), so a ray has 2 * pomdp_r + 2 points (min(H, W) + 1 with full
-    # observability); the device keeps a ray's points in one 64-bit mask
-    if pomdp_r > 31:
-        raise UnsupportedSpec('pomdp_r is limited to 31 (rays of <= 64 points)')
-    if pomdp_r == 0 and min(H, W) > 63:
-        raise UnsupportedSpec('full observability (pomdp_r 0) is limited to levels with min(H, W) <= 63')
+    # observability); rays of up to 64 points render from registers (one 64-bit point mask), longer ones (up to 255
+    # points) on the long-ray render (k_obs_lr: 32-point segments, per-agent tables in HBM)
+    if pomdp_r > 126:
+        raise UnsupportedSpec('pomdp_r is limited to 126 (rays of <= 255 points)')
+    if pomdp_r == 0 and min(H, W) > 254:
+        raise UnsupportedSpec('full observability (pomdp_r 0) is limited to levels with min(H, W) <= 254')
     d = 2 * pomdp_r + 1
     size = pomdp_r ** 2 if pomdp_r else H * W  # LevelParser.size (level_parser.py:44), collection cap (Q16)
 

@@ -92,7 +92,8 @@ def test_bench_launcher_two_ranks_share_gpu(tmp_path):
                        timeout=500)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
-    assert line['n_gpus'] == 2 and line['n_ranks_rccl'] == 2 and 'launcher' in line
+    assert line['n_gpus'] == 2 and line['backend'] == 'gloo' and line['n_ranks_gloo'] == 2 and 'launcher' in line
+    assert 'n_ranks_rccl' not in line  # a gloo group is not labelled RCCL
     assert line['config']['global_batch'] == 2 * 4096 and line['value'] > 0
 
 
@@ -111,4 +112,30 @@ def test_bench_default_lines_run(tmp_path):
     p = line['packed_obs']
     assert p['value'] > 0 and p['fused_proj']['value'] > 0 and p['dense_f32_plus_proj']['value'] > 0
     assert line['cpu_baseline']['value'] > 0 and line['cpu_baseline']['cores'] >= 1
-    assert line['roofline']['frac_sec8d'] > 0 and line['parity']['timed_mode_test']
+    assert line['roofline']['frac'] > 0 and 'frac_sec8d' not in line['roofline'] and line['parity']['timed_mode_test']
+    assert line['roofline']['peak_measured'] > 1000  # the HIP copy kernel's GB/s
+    assert line['backend'] is None and line['n_ranks_rccl'] is None  # bare single process: no group
+
+
+@pytest.mark.timeout(600)
+def test_bench_under_torchrun_one_rank_joins_rccl(tmp_path):
+    """The driver's launch form at N = 1: `python -m torch.distributed.run --nproc-per-node 1 bench.py --gpus 1`,
+    started as a fresh child process (nothing on the GPU in this process's child before the launcher). The rank must
+    join a real nccl (RCCL) process group and run the barriers and the MAX / metrics all-reduces on device tensors."""
+    if not gpu_available():
+        pytest.skip('no GPU')
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    out = tmp_path / 'line.json'
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+                        '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), str(ROOT / 'bench.py'),
+                        '--gpus', '1', '--batch', '4096', '--warmup', '16', '--steps', '32', '--alt-steps', '0',
+                        '--packed-steps', '0', '--no-cpu-baseline'], env=env, capture_output=True, text=True,
+                       timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
+    out.write_text(json.dumps(line))
+    assert line['backend'] == 'nccl' and line['n_ranks_rccl'] == 1 and line['n_gpus'] == 1
+    c = line['collectives']
+    assert c['tensors'].startswith('cuda') and c['metrics_allreduce_episodes'] >= 0
+    assert line['value'] > 0

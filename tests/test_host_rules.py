@@ -211,6 +211,25 @@ class BatteryPostReader(Rule):
         return [TickResult(self.name, validity=True, value=sum(b.charge_level for b in state['Batteries']))]
 
 
+class ReachedPostReader(Rule):
+    """tick_post_step: destination marks (DoneAtDestinationReach 'simultaneous' unmarks them in on_check_done)."""
+    def tick_post_step(self, state):
+        return [TickResult(self.name, validity=True, value=sum(d.was_reached() for d in state['Destinations']))]
+
+
+class ReachedDoneReader(Rule):
+    """on_check_done: the same read inside the done check."""
+    def on_check_done(self, state):
+        _ = [d.reached for d in state['Destinations']]
+        return []
+
+
+class DoorPreMaintReader(Rule):
+    """tick_step: door states (MoveMaintainers opens doors on its routes inside its tick)."""
+    def tick_step(self, state):
+        return [TickResult(self.name, validity=True, value=sum(d.is_open for d in state['Doors']))]
+
+
 class BoundStateReader(Rule):
     """tick_post_step: an agent's state through its battery (WatchCollisions rewrites agent states later)."""
     def tick_post_step(self, state):
@@ -308,3 +327,35 @@ def test_custom_module_cache_is_per_folder(tmp_path, compat_path):
     for _ in range(2):  # the failed import is retried, not served half-initialised from sys.modules
         with pytest.raises(ImportError, match='broken plugin'):
             locate_custom_class('X', tmp_path / 'c')
+
+
+def test_simultaneous_destination_unmark_and_maintainer_doors_refused(tmp_path, compat_path):
+    """DoneAtDestinationReach(condition='simultaneous') unmarks destinations in on_check_done
+    (destinations/rules.py:80-87), so a destination read ahead of it (tick_post_step, or on_check_done before it) is
+    stale; after it the end-of-step value is the reference's. MoveMaintainers opens doors in its tick, so a tick_step
+    door read placed before it is refused too."""
+    import yaml
+    from mfg_amd import info as I
+    from mfg_amd.host_rules import StaleStateError, stale_state
+    from mfg_amd.spec import compile_spec
+    base = yaml.safe_load((ROOT / 'marl-factory-grid_amd' / 'mfg_amd' / 'configs' / 'eight_puzzle.yaml').read_text())
+    rules = dict(base['Rules'])
+    with pytest.raises(StaleStateError, match='DoneAtDestinationReach'):
+        _run_custom(tmp_path, 'eight_puzzle.yaml', {'ReachedPostReader': None, **rules}, 2)
+    with pytest.raises(StaleStateError, match='DoneAtDestinationReach'):
+        _run_custom(tmp_path, 'eight_puzzle.yaml', {'ReachedDoneReader': None, **rules}, 2)
+    spec, out = _run_custom(tmp_path, 'eight_puzzle.yaml', {**rules, 'ReachedDoneReader': None}, 4)
+    assert len(out) == 4
+    slot = spec.host_rules[0][0]
+    assert stale_state(spec, slot, I.DONE) == {}
+    # the maintainer door mutation, statically (grid128 carries MoveMaintainers)
+    g = yaml.safe_load((ROOT / 'marl-factory-grid_amd' / 'mfg_amd' / 'configs' / 'maint_rooms.yaml').read_text())
+    (tmp_path / 'mods').mkdir(exist_ok=True)
+    (tmp_path / 'mods' / 'posreaders.py').write_text(_POS_READERS)
+    rl = list(g['Rules'].items())  # after DoorAutoClose (its own door change is then the hook's), before MoveMaintainers
+    g['Rules'] = dict(rl[:1] + [('DoorPreMaintReader', None)] + rl[1:])
+    p = tmp_path / 'maint.yaml'
+    p.write_text(yaml.safe_dump(g, sort_keys=False))
+    spec = compile_spec(p, custom_modules_path=str(tmp_path / 'mods'))
+    st = stale_state(spec, spec.host_rules[0][0], I.TICK)
+    assert st['Doors'][1] == 'MoveMaintainers' and 'is_open' in st['Doors'][0]

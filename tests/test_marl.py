@@ -271,7 +271,7 @@ def test_fused_gru_window_matches_cells():
         assert torch.allclose(res['fused'][1][k], g, rtol=1e-4, atol=1e-6), (k, (res['fused'][1][k] - g).abs().max())
 
 
-def test_split_k_weight_gradients_match_autograd():
+def test_split_k_weight_gradients_match_autograd(monkeypatch):
     """The learner's split-K layers (_tall_tn weight gradients: _Linear, _Embed with padding_idx, the GRU window)
     give nn.Linear / nn.Embedding / autograd's gradients on a window, forced to split at 64 rows."""
     import mfg_amd.marl as M
@@ -284,12 +284,11 @@ def test_split_k_weight_gradients_match_autograd():
     starts = torch.rand(n, t) < 0.1
     res = {}
     for rows in (64, 1 << 30):
-        M.SPLIT_ROWS = rows
+        monkeypatch.setattr(M, 'SPLIT_ROWS', rows)  # restored by pytest, also on failure
         net.zero_grad()
         out = net.forward_emb(emb, acts, h0, h0, starts=starts)
         (out['logits'].square().sum() + out['critic'].sum()).backward()
         res[rows] = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
-    M.SPLIT_ROWS = 2048
     a, b = res[64], res[1 << 30]
     assert a.keys() == b.keys() and 'action_emb.weight' in a
     assert float(a['action_emb.weight'][0].abs().sum()) == 0.0
@@ -306,7 +305,7 @@ def test_split_k_weight_gradients_match_autograd():
 
 
 @pytest.mark.gpu
-def test_gru_window_kernels_match_tensor_code():
+def test_gru_window_kernels_match_tensor_code(monkeypatch):
     """The learner's GRU window on the GPU through libmfg_hip.so's fused step kernels (mfg_gru_fwd_step /
     mfg_gru_bwd_step, include/mfg_learn.h) against the same window in tensor code, forward and every gradient
     (fp32; the kernels follow the tensor code's formulas, libm exp/tanh may round differently)."""
@@ -322,14 +321,14 @@ def test_gru_window_kernels_match_tensor_code():
     h0 = torch.randn(n, 1, 16, device='cuda')
     starts = torch.rand(n, t, device='cuda') < 0.1
     res = {}
+    orig = M._use_gru_kernels
     for kern in (True, False):
-        M._use_gru_kernels = (lambda x: x.is_cuda and x.dtype == torch.float32) if kern else (lambda x: False)
+        monkeypatch.setattr(M, '_use_gru_kernels', orig if kern else (lambda x: False))  # restored on failure too
         net.zero_grad()
         out = net.forward_emb(emb, acts, h0, h0, starts=starts)
         (out['logits'].square().sum() + out['critic'].sum()).backward()
         res[kern] = ({k: out[k].detach().clone() for k in ('logits', 'critic', 'hidden_actor', 'hidden_critic')},
                      {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None})
-    M._use_gru_kernels = lambda x: x.is_cuda and x.dtype == torch.float32
     for k in res[True][0]:
         assert torch.allclose(res[True][0][k], res[False][0][k], rtol=1e-5, atol=1e-6), k
     for k in res[False][1]:

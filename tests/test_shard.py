@@ -109,7 +109,7 @@ def test_bench_spawns_ranks_and_collects_rank0_line():
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
     assert len(lines) == 1
     d = json.loads(lines[0])
-    assert d['n_gpus'] == 2 and d['n_ranks_rccl'] == 2 and d['dry_run']
+    assert d['n_gpus'] == 2 and d['backend'] == 'gloo' and d['n_ranks_gloo'] == 2 and d['dry_run']
     assert d['env_ranges'] == [[0, 8], [8, 8]]
     assert d['metrics_allreduce'] == 2 * 8 * 5
     assert 'launcher' in d
@@ -123,3 +123,26 @@ def test_bench_refuses_more_gpus_than_visible():
     assert p.returncode == 2
     assert f'{n} GPUs requested, {visible} visible' in p.stderr
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+
+
+def test_bench_under_launcher_world1_joins_a_group():
+    """Under torch.distributed.run with one process (the driver's N = 1 SCALE form) the rank joins a real process
+    group of size 1 (gloo in this CPU rehearsal; nccl on the GPU, tests/test_gpu_ranks.py) instead of skipping it."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.pop('WORLD_SIZE', None)
+    p = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), str(ROOT / 'bench.py'), '--gpus', '1',
+                        '--dry-run', '--steps', '3', '--batch', '8'], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=str(ROOT))
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith('{')][-1])
+    assert d['backend'] == 'gloo' and d['n_ranks_gloo'] == 1 and d['n_gpus'] == 1
+    assert d['metrics_allreduce'] == 8 * 3

@@ -177,19 +177,21 @@ def test_philox_known_answer():
     assert int(philox_u32(0, 0, 0, 0)) == 0x6627E8D5
 
 
-@pytest.mark.parametrize('level,pomdp_r,ok', [('grid128', 31, True), ('grid128', 32, False), ('large_qquad', 0, True),
-                                               ('grid128', 0, False)])
-def test_ray_length_limits(tmp_path, level, pomdp_r, ok):
-    """Rays of up to 64 points (2 * pomdp_r + 2, or min(H, W) + 1 with full observability, Q13): pomdp_r <= 31 and
-    full observability on levels with min(H, W) <= 63 (large_qquad: 47 x 123) compile; longer rays are refused."""
+@pytest.mark.parametrize('level,pomdp_r,pts_range', [('grid128', 31, (33, 64)), ('grid128', 32, (65, 66)),
+                                                     ('large_qquad', 0, (33, 64)), ('grid128', 0, (129, 129)),
+                                                     ('grid128', 126, (254, 254)), ('grid128', 127, None)])
+def test_ray_length_limits(tmp_path, level, pomdp_r, pts_range):
+    """Rays of 2 * pomdp_r + 2 points, or min(H, W) + 1 with full observability (Q13). Up to 64 points render from
+    registers, 65..255 points on the long-ray render (k_obs_lr): pomdp_r <= 126 and full observability on levels with
+    min(H, W) <= 254 compile (grid128 full: 129-point rays); longer rays are refused."""
     from mfg_amd.spec import compile_spec, UnsupportedSpec
     cfg = tmp_path / 'c.yaml'
     cfg.write_text(f"General: {{env_seed: 69, individual_rewards: true, level_name: {level}, pomdp_r: {pomdp_r}}}\n"
                    "Agents: {W: {Actions: [Noop, Move8], Observations: [Walls]}}\nEntities: {}\nRules: {}\n")
-    if ok:
+    if pts_range:
         spec = compile_spec(cfg)
         pts = max(int(b) - int(a) for a, b in zip(spec.c.ray_off[:spec.c.n_rays], spec.c.ray_off[1:spec.c.n_rays + 1]))
-        assert 32 < pts <= 64
+        assert pts_range[0] <= pts <= pts_range[1]
     else:
-        with pytest.raises(UnsupportedSpec, match='64 points|<= 63'):
+        with pytest.raises(UnsupportedSpec, match='255 points'):
             compile_spec(cfg)
