@@ -276,6 +276,8 @@ typedef struct mfg_variant {
   int32_t full_temper;        /* 1: the replay's full MT temper (levels with >= 16384 floor cells) */
   int32_t bfs_hbm;            /* 1: the maintainer BFS scratch in the per-env HBM pool (the grid128 layout) */
   int32_t pairs_lds;          /* > 0: at most this many identifier pairs in LDS, the rest in the HBM spill */
+  int32_t render_slots;       /* > 0: at most this many resident waves in the long-ray render (k_obs_lr), so each
+                                 strides over several envs */
 } mfg_variant;
 int mfg_create_variant(const mfg_spec* spec, int device, int64_t n_envs, const mfg_variant* variant,
                        mfg_engine** out);

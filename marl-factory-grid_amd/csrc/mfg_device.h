@@ -147,6 +147,14 @@ struct MfgDevSpec {
   uint32_t comb_unit_tags[MFG_MAX_AGENTS];
   uint64_t comb_agents[MFG_MAX_AGENTS];
   const MfgLayerRec* lrec;   // [A][lmax] layer records
+  // long-ray render (maxpts == 0: rays of 65..255 points, k_obs_lr): the ray table with 16-bit offsets, and the
+  // per-agent tables (first-visit table, wall suppression, sinks, dirt bitmap, agent masks, dirt map, packed queue:
+  // the same layout as the LDS render's per-wave part) of each resident render wave in HBM instead of LDS
+  const uint32_t* ray_pts16; // [nrays][lrpts] (dx & 0xFFFF) | dy << 16 per point, padded; null unless maxpts == 0
+  int32_t lrpts;             // points per ray slot of ray_pts16 (a multiple of 32)
+  int32_t obs_slots;         // resident long-ray render waves (grid of k_obs_lr), each owning one pool slot
+  int64_t obs_slot_bytes;    // bytes per slot
+  uint8_t* obs_pool;         // [obs_slots][obs_slot_bytes]
   // rules that act in each step phase, in rule order (spawn rules and the like act only at reset)
   int32_t n_ph[3];                       // tick_step, tick_post_step, on_check_done
   uint8_t ph_rule[3][MFG_MAX_RULES];

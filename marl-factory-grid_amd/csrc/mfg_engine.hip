@@ -268,11 +268,11 @@ static int validate_spec(const mfg_spec* s) {
   if (s->n_floor < 1 || s->n_floor > s->H * s->W || !s->floor_cells) return fail("n_floor out of range");
   if (s->n_walls < 0 || s->n_walls > s->H * s->W) return fail("n_walls out of range");
   // the ray radius is the window diameter (Q13): 2 r + 1, or min(H, W) with full observability; a ray holds
-  // radius + 1 points and the walk keeps them in one 32- or 64-bit mask (the per-agent tables must also fit the
-  // LDS, checked below)
-  if (s->pomdp_r < 0 || s->pomdp_r > 31) return fail("engine supports pomdp_r in [0, 31] (rays of <= 64 points)");
-  if (s->pomdp_r == 0 && std::min(s->H, s->W) > 63)
-    return fail("full observability (pomdp_r 0) needs min(H, W) <= 63 (rays of <= 64 points)");
+  // radius + 1 points: up to 64 the walk keeps them in one 32- or 64-bit mask (k_obs), up to 255 the long-ray render
+  // walks 32-point segments (k_obs_lr)
+  if (s->pomdp_r < 0 || s->pomdp_r > 126) return fail("engine supports pomdp_r in [0, 126] (rays of <= 255 points)");
+  if (s->pomdp_r == 0 && std::min(s->H, s->W) > 254)
+    return fail("full observability (pomdp_r 0) needs min(H, W) <= 254 (rays of <= 255 points)");
   for (int a = 0; a < s->n_agents; a++) {
     if (s->n_positions[a] < 0 || s->n_positions[a] > MFG_MAX_POSITIONS) return fail("n_positions out of range");
     for (int k = 0; k < s->n_positions[a]; k++)
@@ -329,7 +329,7 @@ extern "C" int mfg_create_variant(const mfg_spec* s, int device, int64_t n_envs,
   if (!s || !out) return fail("null argument");
   if (n_envs < 1) return fail("n_envs must be >= 1");
   if (validate_spec(s)) return -1;
-  const mfg_variant none{0, 0, 0, 0};
+  const mfg_variant none{0, 0, 0, 0, 0};
   DevGuard g(device);
   return create_impl(s, device, n_envs, v ? *v : none, out);
 }
@@ -377,9 +377,11 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   {  // points per ray (<= fr + 1), rounded up to a compiled k_obs instantiation (DISPATCH_MP)
     int mp = 1;
     for (int r = 0; r < h.nrays; r++) mp = std::max(mp, s->ray_off[r + 1] - s->ray_off[r]);
-    if (mp > 64) { delete e; return fail("rays longer than 64 points"); }
+    if (mp > 255) { delete e; return fail("rays longer than 255 points"); }
     static const int SIZES[] = {4, 6, 8, 10, 12, 14, 16, 18, 24, 32, 48, 64};
+    h.maxpts = 0;  // 0: the long-ray render (k_obs_lr, 32-point segments of a 16-bit ray table)
     for (int k : SIZES) if (k >= mp) { h.maxpts = k; break; }
+    h.lrpts = h.maxpts ? 0 : align_up(mp, 32);
   }
   int lmax = 1;
   for (int a = 0; a < s->n_agents; a++) lmax = s->n_layers[a] > lmax ? s->n_layers[a] : lmax;
@@ -518,19 +520,34 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   h.lds_obs += 12 * h.pairs_lds;
   h.lds_obs_shared = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) + 12 * h.pairs_lds;
   h.lds_obs_wave = align_up(h.lds_obs - h.lds_obs_shared, 16);
+  h.obs_slot_bytes = 0;
+  if (!h.maxpts) {  // long-ray render: the per-agent tables go to an HBM pool slot per resident wave (k_obs_lr)
+    h.obs_slot_bytes = align_up(h.lds_obs_wave, 256);
+    h.lds_obs = h.lds_obs_shared;
+    h.lds_obs_wave = 0;
+  }
   if (h.lds_full > MFG_LDS_MAX || h.lds_obs > MFG_LDS_MAX || h.lds_replay_per_wave > MFG_LDS_MAX) {
     delete e; return fail("env record does not fit one CU's 160 KB of LDS");
   }
   std::vector<int8_t> rp((size_t)h.nrays * h.maxpts * 2, 0);
+  std::vector<uint32_t> rp16((size_t)h.nrays * h.lrpts, 0u);  // long-ray render: dx & 0xFFFF | dy << 16
   std::vector<uint8_t> rlen(h.nrays);
   std::vector<uint64_t> rdiag(h.nrays, 0ull);
   for (int r = 0; r < h.nrays; r++) {
     const int p0 = s->ray_off[r], p1 = s->ray_off[r + 1];
-    if (p1 - p0 > h.maxpts || p1 - p0 > h.fr + 1) { delete e; return fail("ray longer than its radius + 1 points"); }
+    if (p1 - p0 > (h.maxpts ? h.maxpts : h.lrpts) || p1 - p0 > h.fr + 1) {
+      delete e; return fail("ray longer than its radius + 1 points");
+    }
     if (p1 - p0 < 1 || s->ray_pts[2 * p0] != 0 || s->ray_pts[2 * p0 + 1] != 0) {  // k_obs relies on it
       delete e; return fail("every ray must start at the origin (bresenham_loop, ray_caster.py:141-199)");
     }
     rlen[r] = (uint8_t)(p1 - p0);
+    if (!h.maxpts) {  // (the long-ray walk tests diagonal steps from consecutive points itself)
+      for (int p = p0; p < p1; p++)
+        rp16[(size_t)r * h.lrpts + (p - p0)] =
+            ((uint32_t)s->ray_pts[2 * p] & 0xFFFFu) | ((uint32_t)s->ray_pts[2 * p + 1] << 16);
+      continue;
+    }
     for (int p = p0 + 1; p < p1; p++)
       if (s->ray_pts[2 * p] != s->ray_pts[2 * p - 2] && s->ray_pts[2 * p + 1] != s->ray_pts[2 * p - 1])
         rdiag[r] |= 1ull << (p - p0);
@@ -548,11 +565,13 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   rc |= upload(e, rp.data(), rp.size(), &h.ray_pts);
   rc |= upload(e, rlen.data(), rlen.size(), &h.ray_len);
   rc |= upload(e, rdiag.data(), rdiag.size(), &h.ray_diag);
+  h.ray_pts16 = nullptr;
+  if (!h.maxpts) rc |= upload(e, rp16.data(), rp16.size(), &h.ray_pts16);
   {  // static light-blocking table per (origin floor cell, ray): walls only; door-dependent points flagged
     // (32-bit point masks: rays of up to 32 points; longer rays test every point against the cell map)
     const size_t n = (size_t)s->n_floor * h.nrays * 3;
     h.ray_static = nullptr;
-    if (n * 4 <= ((size_t)256 << 20) && h.maxpts <= 32) {
+    if (n * 4 <= ((size_t)256 << 20) && h.maxpts && h.maxpts <= 32) {
       std::vector<uint32_t> rs(n, 0u);
       auto wall = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && s->level[x * s->W + y] == 1; };
       auto door = [&](int x, int y) { return x >= 0 && y >= 0 && x < s->H && y < s->W && door_of[x * s->W + y] != 0xFF; };
@@ -710,6 +729,19 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     const int obs_per_cu = std::max(1, std::min(32 / ow, (int)(MFG_LDS_MAX / ((size_t)h.lds_obs * ow))));
     e->obs_list_blocks = obs_per_cu * std::max(1, n_cu);
   }
+  if (!h.maxpts) {  // long-ray render: one HBM pool slot per resident wave (one wave per SIMD)
+    h.obs_slots = (int)std::max<long long>(1, std::min<long long>(n_envs, 4LL * e->n_cu));
+    if (v.render_slots > 0) h.obs_slots = std::min(h.obs_slots, (int)v.render_slots);  // mfg_variant (tests)
+    void* pool = nullptr;
+    if (hipMalloc(&pool, (size_t)h.obs_slot_bytes * (size_t)h.obs_slots) != hipSuccess) {
+      delete e; return fail("long-ray render pool allocation failed");
+    }
+    e->d_bufs.push_back(pool);
+    h.obs_pool = (uint8_t*)pool;
+    if (hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
+      delete e; return fail("spec upload failed");
+    }
+  }
   *out = e;
   return 0;
 }
@@ -766,7 +798,12 @@ static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipS
                                const int32_t* list) {
   ObsLaunch L;
   L.mw = e->obs_nwv > 1;
-  if (L.mw) {  // one env per workgroup
+  if (MP == 0) {  // long-ray render: a resident grid, workgroup g owns HBM pool slot g (k_obs_lr)
+    L.mw = false;
+    L.W = 1;
+    L.grid = (unsigned)e->h.obs_slots;
+    L.lds = (size_t)e->h.lds_obs;
+  } else if (L.mw) {  // one env per workgroup
     L.W = e->obs_nwv;
     L.lds = (size_t)e->h.lds_obs_shared + (size_t)L.W * e->h.lds_obs_wave;
     const long long per_cu = std::max<long long>(1, (long long)(MFG_LDS_MAX / L.lds));
@@ -786,6 +823,7 @@ static hipError_t launch_obs_t(mfg_engine* e, OT* obs, const ObsPacked& pk, hipS
 
 #define DISPATCH_MP(MPVAL, CALL) \
   switch (MPVAL) {               \
+    case 0: { constexpr int MP = 0; CALL; } break; \
     case 4: { constexpr int MP = 4; CALL; } break; \
     case 6: { constexpr int MP = 6; CALL; } break; \
     case 8: { constexpr int MP = 8; CALL; } break; \

@@ -2415,16 +2415,22 @@ __device__ int build_id_pairs(const Env& e, const PairList& pairs) {
   return n < cap ? n : cap;
 }
 
-struct Sup {  // per-agent suppression sets from the identifier dedupe
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// the render's per-agent tables: LDS, or (long-ray render, k_obs_lr) the wave's HBM pool slot
+template <bool LR>
+using obs_u32 = typename std::conditional<LR, uint32_t, lds_u32>::type;
+template <typename DP>
+struct SupT {  // per-agent suppression sets from the identifier dedupe
   u64 items, pods, drops, dests, doors, machines, maints;
   uint8_t* wsup;   // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
-  __attribute__((address_space(3))) uint32_t* dsup;  // dirt slots: LDS bitmap [dirt_cap / 32]
+  DP* dsup;        // dirt slots: bitmap [dirt_cap / 32] (LDS; HBM in the long-ray render)
   int wx0, wy0, oh, ow, W;  // window origin cell and shape
   __device__ __forceinline__ bool dirt_sup(int i) const {
     return ((dsup[i >> 5] >> (i & 31)) & 1u) != 0;
   }
 };
-__device__ __forceinline__ void sup_add(Sup& s, int code, int xy, int lane) {
+template <typename DP>
+__device__ __forceinline__ void sup_add(SupT<DP>& s, int code, int xy, int lane) {
   const int kind = code >> 12, slot = code & 0xFFF;
   const u64 bit = 1ull << (slot & 63);
   switch (kind) {
@@ -2460,9 +2466,25 @@ struct ObsPacked {
 // MW: the env's workgroup has nwv waves (wave wv renders agents wv, wv + nwv, ...); they share the lean record,
 // the cell map and the identifier pairs, each has its own per-agent tables after the shared part
 // (S->lds_obs_shared + wv * S->lds_obs_wave)
+// MAXPTS == 0 (LR): the long-ray render (rays of 65..255 points, k_obs_lr): each ray is walked in 32-point segments
+// from the 16-bit ray table, and the per-agent tables (first-visit table, wall suppression, sinks, dirt bitmap,
+// agent masks, dirt map, packed queue) live in the wave's HBM pool slot `slot` instead of LDS.
+template <bool LR>
+__device__ __forceinline__ void tbl_sync() {
+  if constexpr (LR) {  // tables in HBM: stores and L2 atomics complete, and no stale L1 line is read afterwards
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    wave_sync();
+  }
+}
 template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT, bool MW>
-__device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPacked& pk, int wv, int nwv) {
+__device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPacked& pk, int wv, int nwv,
+                          int slot = 0) {
   SpecP S = e.S;
+  constexpr bool LR = MAXPTS == 0;
+  constexpr int RMP = LR ? 2 : MAXPTS;  // RayLane width (unused by the long-ray walk)
+  typedef obs_u32<LR> tu32;
   // window: oh x ow cells from (wx0, wy0) = agent - r, or the whole level at (0, 0) when pomdp_r == 0
   // (observation_builder.py:152-158); rays and the first-visit table have radius fr (Q13)
   const int A = S->A, H = S->s.H, W = S->s.W, oh = S->oh, ow = S->ow, dd = S->dd, fr = S->fr;
@@ -2493,23 +2515,23 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   // first-visit table: (2d+1)^2 cells around the ray origin, min over visible (ray, point) of
   // ray << 5 | point (ray << 6 | point for rays longer than 32 points); it gives both the window visibility and the
   // dedupe order (Q14)
-  uint32_t* fv = (uint32_t*)(e.scratch + 3 * S->pairs_lds + (MW ? wv * (S->lds_obs_wave >> 2) : 0));
+  uint32_t* fv = LR ? (uint32_t*)(S->obs_pool + (size_t)slot * (size_t)S->obs_slot_bytes)
+                    : (uint32_t*)(e.scratch + 3 * S->pairs_lds + (MW ? wv * (S->lds_obs_wave >> 2) : 0));
   const int fw = 2 * fr + 1;
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
   // dirt suppression bitmap for groups wider than a wave: after the per-lane sink words of the ray walk
-  typedef __attribute__((address_space(3))) uint32_t lds_u32;
-  lds_u32* dsup = (lds_u32*)((uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE);
+  tu32* dsup = (tu32*)((uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE);
   const int ndsup = S->dirt_cap >> 5;
   // agents on each window cell: [dd][2] u32 (bit b = agent b), filled by a lane-per-agent scatter
-  lds_u32* amw = dsup + ndsup;
+  tu32* amw = dsup + ndsup;
   // window dirt map (specs with dirt): per window cell 1 + the index of the last present, non-suppressed pile on
   // it, built per agent from the pile table (lane = pile), so the placement reads a cell's pile instead of
   // scanning every pile per 64-cell block (C5: up to 384 piles)
-  lds_u32* wdirt = amw + 2 * dd;
+  tu32* wdirt = amw + 2 * dd;
   // packed mode: queue of the agent row's nonzero entries awaiting the fused projection ([64] flat index, [64] value);
   // the weight rows of up to 4 entries are loaded together, so their L2 latencies overlap instead of chaining
-  lds_u32* pq = wdirt + (DIRT ? dd : 0);
+  tu32* pq = wdirt + (DIRT ? dd : 0);
   constexpr bool has_dirt = DIRT;  // S->dirt_cap != 0 (a template parameter: the register budget of k_obs)
   const float invW = 1.0f / (float)W;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
@@ -2522,9 +2544,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   const int agx = agp / W, agy = agp % W, orgx = org_l / W, orgy = org_l % W;
   // the first pass's rays are agent independent: loaded once per render, not once per agent, where the
   // registers they then hold across the agent loop do not cost occupancy (short rays, dense obs)
-  constexpr bool HOIST_RAYS = MAXPTS <= 8 && PK == 0;  // (packed renders: per agent, measured faster)
-  constexpr bool PREFETCH_RS = MAXPTS <= 8 && PK != 2;
-  RayLane<MAXPTS> ray0;
+  constexpr bool HOIST_RAYS = !LR && MAXPTS <= 8 && PK == 0;  // (packed renders: per agent, measured faster)
+  constexpr bool PREFETCH_RS = !LR && MAXPTS <= 8 && PK != 2;
+  RayLane<RMP> ray0;
   if constexpr (HOIST_RAYS) ray0.load(S, lane);
   // ... and their static light-blocking words are fetched one agent ahead (an L2 round trip behind a
   // dependent cell_f load, hidden under the previous agent's dedupe and placement)
@@ -2554,7 +2576,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     for (int i = lane; i < 2 * dd; i += MFG_WAVE) amw[i] = 0u;
     if (has_dirt)
       for (int i = lane; i < dd; i += MFG_WAVE) wdirt[i] = 0u;
-    wave_sync();
+    tbl_sync<LR>();
     if (lane < A) {  // scatter the agents into the window's agent masks
       const int wx = agx - wx0, wy = agy - wy0;
       if ((unsigned)wx < (unsigned)oh && (unsigned)wy < (unsigned)ow)
@@ -2565,18 +2587,64 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0u;
     if (0)
 #endif
+    if constexpr (LR) {
+      // long rays: each lane walks its ray in 32-point segments (points from the 16-bit table, dx | dy << 16),
+      // carrying whether the walk has stopped and the previous point (the diagonal cut of a segment's first point);
+      // per segment the same branch-free walk as below, first-visit rank = ray << 8 | point
+      for (int pass = 0; pass < npass; pass++) {
+        const int ray_id = pass * MFG_WAVE + lane;
+        const bool has = ray_id < S->nrays;
+        const int len = has ? (int)S->ray_len[ray_id] : 0;
+        const uint32_t* rp = S->ray_pts16 + (size_t)(has ? ray_id : 0) * S->lrpts;
+        uint32_t* sink = (uint32_t*)(wsup + ((dd + 15) & ~15)) + lane;
+        bool stopped = false;
+        int pdx = 0, pdy = 0;
+        for (int s0 = 0; s0 < S->lrpts; s0 += 32) {
+          uint32_t pt[32];
+#pragma unroll
+          for (int q = 0; q < 32; q++) pt[q] = rp[s0 + q];
+          uint32_t blkm = 0u, cutm = 0u;
+#pragma unroll
+          for (int q = 0; q < 32; q++) {
+            const int dx = (int)(int16_t)(pt[q] & 0xFFFFu), dy = (int)(int16_t)(pt[q] >> 16);
+            const int qdx = q ? (int)(int16_t)(pt[q - 1] & 0xFFFFu) : pdx, qdy = q ? (int)(int16_t)(pt[q - 1] >> 16) : pdy;
+            const int x = ox + dx, y = oy + dy;
+            blkm |= light_block_bf<MM>(e, x, y) ? (1u << q) : 0u;
+            // a diagonal step from the previous point is cut when both orthogonal neighbours block light
+            // (ray_caster.py:89-96)
+            const bool dg = (s0 + q > 0) & (dx != qdx) & (dy != qdy);
+            const bool c = dg & light_block_bf<MM>(e, x, oy + qdy) & light_block_bf<MM>(e, ox + qdx, y);
+            cutm |= c ? (1u << q) : 0u;
+          }
+          pdx = (int)(int16_t)(pt[31] & 0xFFFFu);
+          pdy = (int)(int16_t)(pt[31] >> 16);
+          const int rem = len - s0;
+          const uint32_t lenm = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+          const uint32_t stopm = (blkm | cutm) & lenm;
+          const uint32_t walked = stopped ? 0u : (stopm ? (((stopm & (0u - stopm)) << 1) - 1u) & lenm : lenm);
+          const uint32_t vism = walked & ~cutm;
+          stopped |= stopm != 0u;
+#pragma unroll
+          for (int q = 0; q < 32; q++) {
+            const int dx = (int)(int16_t)(pt[q] & 0xFFFFu), dy = (int)(int16_t)(pt[q] >> 16);
+            const bool vq = ((vism >> q) & 1u) && (s0 + q > 0);  // the origin (point 0) is stored once below
+            atomicMin(vq ? &fv[(dx + fr) * fw + dy + fr] : sink, (uint32_t)((ray_id << 8) + s0 + q));
+          }
+        }
+      }
+    } else
     for (int pass = 0; pass < npass; pass++) {
       const int ray_id = pass * MFG_WAVE + lane;
-      RayLane<MAXPTS> ray;
+      RayLane<RMP> ray;
       if (HOIST_RAYS && pass == 0) ray = ray0;
       else ray.load(S, ray_id);
       // branch-free: every point tests its cell and (from p = 1) both corner cells; the static diagonal
       // mask keeps the corner test only on diagonal steps: cut when both orthogonal neighbours block
       // light (ray_caster.py:89-96)
-      typedef typename RayLane<MAXPTS>::PM PM;
+      typedef typename RayLane<RMP>::PM PM;
       constexpr int NB = 8 * (int)sizeof(PM);
       PM blkm = 0, cutm = 0;
-      if (MAXPTS <= 32 && ofl >= 0) {  // (no static table for rays longer than 32 points: ofl is -1 there)
+      if (RMP <= 32 && ofl >= 0) {  // (no static table for rays longer than 32 points: ofl is -1 there)
         // the wall part from the per-origin table; only points next to doors are tested here (the door's
         // present/closed state lives in the cell map)
         uint32_t dyn;
@@ -2605,7 +2673,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         }
       } else {
 #pragma unroll
-        for (int p = 0; p < MAXPTS; p++) {
+        for (int p = 0; p < RMP; p++) {
           const int x = ox + ray.dx(p), y = oy + ray.dy(p);
           blkm |= light_block_bf<MM>(e, x, y) ? ((PM)1 << p) : (PM)0;
           if (p > 0) {
@@ -2626,14 +2694,14 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // point 0 of every ray is the origin (checked at mfg_create) and always visible: its entry is
       // ray 0's rank 0, stored once below instead of a 64-lane same-address atomic
 #pragma unroll
-      for (int p = 1; p < MAXPTS; p++)
+      for (int p = 1; p < RMP; p++)
         atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + fr) * fw + ray.dy(p) + fr] : sink,
-                  (uint32_t)((ray_id << RayLane<MAXPTS>::RSH) + p));
+                  (uint32_t)((ray_id << RayLane<RMP>::RSH) + p));
     }
     if (lane == 0) fv[fr * fw + fr] = 0u;
-    wave_sync();
+    tbl_sync<LR>();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
-    Sup sup;
+    SupT<tu32> sup;
     sup.items = sup.pods = sup.drops = sup.dests = sup.doors = sup.machines = sup.maints = 0;
     sup.wx0 = wx0; sup.wy0 = wy0; sup.oh = oh; sup.ow = ow; sup.W = W;
     sup.wsup = wsup;
@@ -2662,7 +2730,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         else sup_add(sup, codes & 0xFFFF, rl(pA, L), lane);
       }
     }
-    wave_sync();
+    tbl_sync<LR>();
     if (has_dirt) {
       // clean_up piles on window cells, in table order: the last one wins (the sequential scan it replaces
       // kept the last matching pile's amount); cell / W through a float reciprocal (exact for cells < 2^16)
@@ -2676,7 +2744,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
             !sup.dirt_sup(i))
           atomicMax((uint32_t*)&wdirt[px * ow + py], (uint32_t)(i + 1));
       }
-      wave_sync();
+      tbl_sync<LR>();
     }
     OT* out_a = PK ? nullptr : out_env + (size_t)a * S->obs_agent_stride;
     const int nl = S->s.n_layers[a];
@@ -2832,7 +2900,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
           if (nzm) {
             const int nb = popc(nzm);
             if (nq + nb > MFG_WAVE) {
-              wave_sync();
+              tbl_sync<LR>();
               flush();
             }
             if (nz) {
@@ -2871,7 +2939,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     }
     if constexpr (PK) {
       if (nq) {
-        wave_sync();
+        tbl_sync<LR>();
         flush();
       }
       const int pcount = qbase;
@@ -3216,7 +3284,7 @@ k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B, int rd_slot) {
 // One env's render (observation_builder.py:138-235) in its LDS slice.
 template <int MAXPTS, typename OT, bool MM, int PK, bool DIRT, bool MW = false>
 __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* state, long long env, OT* obs,
-                                        ObsPacked pk, int wv = 0, int nwv = 1) {
+                                        ObsPacked pk, int wv = 0, int nwv = 1, int slot = 0) {
   // slice: [lean record][cell map][pairs] (+ per-wave tables, build_obs)
   Env e;
   e.S = S; e.lds = slice; e.stab = nullptr;
@@ -3239,9 +3307,9 @@ __device__ __forceinline__ void obs_env(SpecP S, uint8_t* slice, const uint8_t* 
     pk.val = pk.val ? pk.val + ea * pk.cap : nullptr;
     pk.cnt = pk.cnt ? pk.cnt + ea : nullptr;
     pk.emb = pk.emb ? pk.emb + ea * pk.E : nullptr;
-    build_obs<MAXPTS, OT, MM, PK, DIRT, MW>(e, nullptr, pg, pk, wv, nwv);
+    build_obs<MAXPTS, OT, MM, PK, DIRT, MW>(e, nullptr, pg, pk, wv, nwv, slot);
   } else {
-    build_obs<MAXPTS, OT, MM, PK, DIRT, MW>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg, pk, wv, nwv);
+    build_obs<MAXPTS, OT, MM, PK, DIRT, MW>(e, obs + (size_t)env * S->A * S->obs_agent_stride, pg, pk, wv, nwv, slot);
   }
   // k_obs reads only [0, o_mt) of the record and stores only this word: the replay of the same call may run beside it
   // on the engine's second stream and writes H_DEBT / H_MT_IDX (single words) and [o_mt, o_perm + 2 nf) (replay_env)
@@ -3286,6 +3354,23 @@ static __global__ void __launch_bounds__(8 * 64) k_obs_mw_list(const MfgDevSpec*
     const long long env = uni(list[2 + q]);
     if (env >= 0 && env < B)
       obs_env<MAXPTS, OT, MM, PK, DIRT, true>(S, smem, state, env, obs, pk, uni(threadIdx.x >> 6), blockDim.x >> 6);
+  }
+}
+// Long-ray render (rays of 65..255 points: pomdp_r 32..126, full observability on levels with min(H, W) 64..254): a
+// resident grid of single-wave workgroups strides over every env (skip: envs left to the list render) or over a done
+// list; workgroup g owns HBM pool slot g for its per-agent tables (build_obs, LR), its LDS slice holds the lean record,
+// the cell map and the identifier pairs.
+template <typename OT, bool MM, int PK, bool DIRT>
+static __global__ void __launch_bounds__(MFG_WAVE) k_obs_lr(const MfgDevSpec* S_, const uint8_t* state, long long B,
+                                                            OT* obs, ObsPacked pk, const uint8_t* skip,
+                                                            const int32_t* list) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  SpecP S = (SpecP)S_;
+  const long long n = list ? min((long long)uni(list[0]), B) : B;
+  for (long long q = blockIdx.x; q < n; q += gridDim.x) {
+    const long long env = list ? (long long)uni(list[2 + q]) : q;
+    if (env < 0 || env >= B || (!list && skip && skip[env])) continue;
+    obs_env<0, OT, MM, PK, DIRT>(S, smem, state, env, obs, pk, 0, 1, (int)blockIdx.x);
   }
 }
 // Render of the envs of a done list (rd_list row: [0] = count, [2..] = envs): a resident grid strides over it.
@@ -3586,6 +3671,11 @@ hipError_t launch_obs_inst(const ObsLaunch& L, OT* obs, const ObsPacked& pk, hip
 #define MFG_OBS_LAUNCH_IF(MMV, DV)                                                                               \
   if (L.mm == MMV && L.dirt == DV) {                                                                             \
     bool mw_done = false;                                                                                        \
+    if constexpr (MP == 0) {                                                                                     \
+      mw_done = true;                                                                                            \
+      hipLaunchKernelGGL((k_obs_lr<OT, MMV, PK, DV>), dim3(L.grid), dim3(64), L.lds, st, L.d_spec, L.d_state,    \
+                         L.B, obs, pk, skip, list);                                                              \
+    }                                                                                                            \
     if constexpr (MP >= 10) {                                                                                    \
       if (L.mw) {                                                                                                \
         mw_done = true;                                                                                          \
@@ -3597,7 +3687,7 @@ hipError_t launch_obs_inst(const ObsLaunch& L, OT* obs, const ObsPacked& pk, hip
                              L.d_state, L.B, obs, pk, skip);                                                     \
       }                                                                                                          \
     }                                                                                                            \
-    if (!mw_done) {                                                                                              \
+    if constexpr (MP != 0) if (!mw_done) {                                                                       \
       if (list)                                                                                                  \
         hipLaunchKernelGGL((k_obs_list<MP, OT, MMV, PK, DV>), dim3(L.grid), dim3(L.W * 64), L.lds, st, L.d_spec, \
                            L.d_state, L.B, obs, pk, list);                                                       \

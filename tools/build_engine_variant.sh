@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 CSRC=marl-factory-grid_amd/csrc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC"
 mkdir -p build/obj build/ablate
-for u in mfg_obs_a mfg_obs_b mfg_obs_c mfg_obs_d mfg_obs_e mfg_learn; do
+for u in mfg_obs_a mfg_obs_b mfg_obs_c mfg_obs_d mfg_obs_e mfg_obs_f mfg_learn; do
   if [ ! -f build/obj/$u.o ] || [ $CSRC/mfg_kernels.h -nt build/obj/$u.o ] || [ $CSRC/$u.hip -nt build/obj/$u.o ]; then
     /opt/rocm/bin/hipcc $FLAGS -c -o build/obj/$u.o $CSRC/$u.hip &
   fi
@@ -21,6 +21,6 @@ wait
 for arg in "$@"; do
   name=${arg%%=*}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/ablate/libmfg_hip_$name.so build/obj/engine_$name.o \
-    build/obj/mfg_obs_a.o build/obj/mfg_obs_b.o build/obj/mfg_obs_c.o build/obj/mfg_obs_d.o build/obj/mfg_obs_e.o build/obj/mfg_learn.o
+    build/obj/mfg_obs_a.o build/obj/mfg_obs_b.o build/obj/mfg_obs_c.o build/obj/mfg_obs_d.o build/obj/mfg_obs_e.o build/obj/mfg_obs_f.o build/obj/mfg_learn.o
 done
 ls -la build/ablate
