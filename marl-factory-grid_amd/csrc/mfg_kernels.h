@@ -18,7 +18,7 @@
 // tests force exact alternative paths through the test-only mfg_create_variant, include/mfg.h):
 //   MFG_RESET_OVERLAP      resets + their renders on a second stream beside the render (below)
 //   MFG_REPLAY2            the two-wave replay: 1 by occupancy (default), 2 always (the parity suite runs it on C2-C4)
-//   MFG_ABLATE_*           timing-only ablations, results NOT exact (tools/build_ablation.sh,
+//   MFG_ABLATE_*           timing-only ablations, results NOT exact (tools/build_ablation.sh, tools/build_obs_variant.sh,
 //                          profiles/r04_replay_ablation.json)
 #ifndef MFG_RESET_OVERLAP
 // mfg_step with auto-reset: the resets + their renders on a second stream beside the other envs' render.
@@ -2570,6 +2570,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     const int wx0 = full ? 0 : ax - S->r, wy0 = full ? 0 : ay - S->r;
     // origin floor index (static table)
     const int ofl = PREFETCH_RS ? pf_ofl : (S->ray_static ? uni((int)S->cell_f[ox * W + oy]) : -1);
+#ifdef MFG_ABLATE_OB_NOINIT  // timing only: the per-agent tables are cleared for the first agent only
+    if (a == (MW ? wv : 0))
+#endif
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
@@ -2827,6 +2830,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       uint32_t tags = m & ((wall_sup ? 0u : CM_WALL) | CM_DOOR | CM_ITEM | CM_POD | CM_DROP | CM_DIRT | CM_DEST);
       if (MM) tags |= (m >> 1) & ((1u << MFG_TAG_MACHINES) | (1u << MFG_TAG_MAINTAINERS));
       // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
+#ifdef MFG_ABLATE_OB_NORESUP  // timing only: the identifier-dedupe suppressions are not applied to the placement
+      sup.doors = sup.items = sup.pods = sup.drops = sup.dests = sup.machines = sup.maints = 0;
+#endif
       if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
       auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
         if (!sm) return;

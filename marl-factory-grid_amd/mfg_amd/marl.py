@@ -510,11 +510,15 @@ class BatchedA2C:
     the render's own fused output (every slot was rendered with the current weights; ``engine_emb=False``
     re-evaluates it by ``embedding_bag`` over the stored entries), its backward runs on the stored entries. No host
     synchronisation inside ``step``;
-    ``learn`` syncs once when ``check_cap`` is set (truncated packed rows raise)."""
+    ``learn`` syncs once when ``check_cap`` is set (truncated packed rows raise).
+
+    ``graph=True``: the update (loss, backward, gradient clipping, RMSprop step and the window slide, ~1,300 launches)
+    is captured once as a HIP graph after two eager warm-up updates on a side stream and replayed from then on (one
+    launch per update); the optimizer then keeps its step counters on the device (``capturable``)."""
 
     def __init__(self, factory, net=None, n_steps=5, gamma=0.99, entropy_coef=0.01, vf_coef=0.5, gae_coef=0.0,
                  lr=3e-4, cap=32, obs_emb_size=96, action_emb_size=16, hidden_size=64, use_agent_embedding=False,
-                 check_cap=True, generator=None, engine_emb=True):
+                 check_cap=True, generator=None, engine_emb=True, graph=False):
         from .engine import PackedObs
         self.f = factory
         eng = factory.engine
@@ -537,7 +541,9 @@ class BatchedA2C:
             kdim, self.n_actions, obs_emb_size, action_emb_size, hidden_size, hidden_size, self.A,
             use_agent_embedding=use_agent_embedding)
         self.net.to(self.dev)
-        self.opt = torch.optim.RMSprop(self.net.parameters(), lr=lr, eps=1e-5)
+        self.graph = bool(graph)
+        self.opt = torch.optim.RMSprop(self.net.parameters(), lr=lr, eps=1e-5, capturable=self.graph)
+        self._graph, self._warm = None, 0
         self.T, self.gamma, self.entropy_coef, self.vf_coef, self.gae_coef = n_steps, gamma, entropy_coef, \
             vf_coef, gae_coef
         self.check_cap = check_cap
@@ -554,7 +560,8 @@ class BatchedA2C:
         H = self.net.hidden_size_actor
         self.h0a = torch.zeros((N, 1, H), device=dev)  # hidden state fed at entry 0 of the window
         self.h0c = torch.zeros((N, 1, self.net.hidden_size_critic), device=dev)
-        self.ha, self.hc = self.h0a.clone(), self.h0c.clone()
+        self.ha, self.hc = self.h0a.clone(), self.h0c.clone()  # persistent: updated in place (graph inputs)
+        self.last_loss = torch.zeros((), device=dev)
         self.agent_ids = torch.arange(self.A, device=dev).repeat(self.B)
         self.t = 0
         self.updates = 0
@@ -591,8 +598,8 @@ class BatchedA2C:
         self.act_in[t + 1].copy_(torch.where(d.view(-1, 1), torch.full_like(a.view(self.B, self.A), -1),
                                              a.view(self.B, self.A)))
         keep = (~d).repeat_interleave(self.A).view(self.N, 1, 1).to(self.ha.dtype)
-        self.ha = out['hidden_actor'] * keep
-        self.hc = out['hidden_critic'] * keep
+        torch.mul(out['hidden_actor'], keep, out=self.ha)
+        torch.mul(out['hidden_critic'], keep, out=self.hc)
         self.episodes += d.sum()
         self.reward_sum += self.rew[t].sum()
         self.t += 1
@@ -630,25 +637,47 @@ class BatchedA2C:
         """One A2C update on the window (base_ac.py:200-225), then slide: o_T becomes o_0."""
         if self.check_cap:
             self.pobs.check()
+        if not self.graph:
+            self._update()
+        elif self._graph is not None:
+            self._graph.replay()
+        elif self._warm < 2:  # eager warm-up on a side stream (lazy library state outside the capture)
+            side = torch.cuda.Stream(self.dev)
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(side):
+                self._update()
+            torch.cuda.current_stream(self.dev).wait_stream(side)
+            self._warm += 1
+        else:
+            g = torch.cuda.CUDAGraph()
+            self.opt.zero_grad(set_to_none=True)
+            with torch.cuda.graph(g):
+                self._update()
+            self._graph = g
+            g.replay()  # capture records only: this update runs here
+        self.updates += 1
+        self.t = 0
+
+    def _update(self):
+        """The update and the slide on static buffers (the body HIP-graph captured when graph=True)."""
         with torch.enable_grad():
             loss = self.loss()
-            self.opt.zero_grad()
+            self.opt.zero_grad(set_to_none=True)
             loss.backward()
             torch.nn.utils.clip_grad_norm_(self.net.parameters(), 0.5)
             self.opt.step()
-        self.last_loss = loss.detach()
-        self.updates += 1
         with torch.no_grad():
+            self.last_loss.copy_(loss.detach())
             T = self.T
             self.pobs.idx[0].copy_(self.pobs.idx[T])
             self.pobs.val[0].copy_(self.pobs.val[T])
             self.pobs.count[0].copy_(self.pobs.count[T])
             self.act_in[0].copy_(self.act_in[T])
-            self.h0a, self.h0c = self.ha.clone(), self.hc.clone()
+            self.h0a.copy_(self.ha)
+            self.h0c.copy_(self.hc)
             # new weights: the engine projects with them from now on; o_0's projection is redone here
             self.pobs.set_projection(self.net.obs_proj.weight, self.net.obs_proj.bias)
             self.pobs.emb[0].copy_(_project_dense(self.pobs.idx[0], self.pobs.val[0], self.net.obs_proj))
-        self.t = 0
 
     def train(self, n_updates):
         for _ in range(n_updates * self.T):

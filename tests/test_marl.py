@@ -194,6 +194,30 @@ def test_batched_a2c_trains_on_device():
 
 
 @pytest.mark.gpu
+def test_batched_a2c_graph_update_matches_eager():
+    """graph=True (the update captured once as a HIP graph after two eager warm-up updates, then replayed) trains
+    like the eager loop: same sampled actions (same generator seeds), the same losses and weights after 5 updates
+    within f32 tolerance (the capturable RMSprop keeps its step count on the device)."""
+    from mfg_amd.factory import BatchedFactory
+    from mfg_amd.marl import BatchedA2C
+    res = {}
+    for graph in (False, True):
+        f = BatchedFactory('large8.yaml', 256, seed_base=5)
+        torch.manual_seed(11)
+        tr = BatchedA2C(f, n_steps=5, generator=torch.Generator(device='cuda').manual_seed(2), graph=graph)
+        losses = [float(tr.train(1)) for _ in range(5)]
+        assert tr.updates == 5 and (tr._graph is not None) == graph
+        res[graph] = (losses, {n: p.detach().clone() for n, p in tr.net.named_parameters()},
+                      tr.pobs.emb[0].clone())
+        f.close()
+    for a, b in zip(res[False][0], res[True][0]):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (res[False][0], res[True][0])
+    for n, p in res[False][1].items():
+        assert torch.allclose(res[True][1][n], p, rtol=1e-4, atol=1e-5), n
+    assert torch.allclose(res[True][2], res[False][2], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
 def test_a2c_loss_from_engine_projection_matches_gather():
     """The learner's obs_proj forward taken from the render's fused output gives the embedding_bag loss and
     gradients (f32 tolerance): every window slot was rendered with the current weights."""

@@ -20,13 +20,14 @@ def main():
     ap.add_argument('--batch', type=int, default=8192)
     ap.add_argument('--updates', type=int, default=20)
     ap.add_argument('--n-steps', type=int, default=5)
+    ap.add_argument('--eager', action='store_true', help='no HIP-graph capture of the update (BatchedA2C graph=False)')
     args = ap.parse_args()
     import torch
     from mfg_amd.factory import BatchedFactory
     from mfg_amd.marl import BatchedA2C
     f = BatchedFactory(args.config, args.batch, seed_base=0)
-    tr = BatchedA2C(f, n_steps=args.n_steps, check_cap=True)
-    tr.train(2)  # warm-up (allocations, kernels)
+    tr = BatchedA2C(f, n_steps=args.n_steps, check_cap=True, graph=not args.eager)
+    tr.train(3)  # warm-up (allocations, kernels; graph=True: two eager updates, then the capture)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss = tr.train(args.updates)
@@ -43,6 +44,7 @@ def main():
     torch.cuda.synchronize()
     env_el = time.perf_counter() - t1
     out = {"what": "on-GPU A2C (BatchedA2C): act + mfg_step(packed obs, fused obs_proj) + learn every n_steps",
+           "update": "eager" if args.eager else "HIP graph (captured once, replayed per update)",
            "config": args.config, "envs": args.batch, "agents": f.spec.n_agents, "updates": args.updates,
            "n_steps": args.n_steps, "env_steps_per_s": round(args.batch * steps / el, 1),
            "agent_steps_per_s": round(args.batch * f.spec.n_agents * steps / el, 1),
