@@ -2466,6 +2466,15 @@ struct ObsPacked {
 // MW: the env's workgroup has nwv waves (wave wv renders agents wv, wv + nwv, ...); they share the lean record,
 // the cell map and the identifier pairs, each has its own per-agent tables after the shared part
 // (S->lds_obs_shared + wv * S->lds_obs_wave)
+#ifndef MFG_OBS_FLAT
+// dense obs: the placement stashes each window cell's tags, visible agent mask and pile index, then writes the agent's
+// [nl][dd] block as consecutive 64-value runs (lane = element) instead of one partial run per layer (0: per layer)
+#define MFG_OBS_FLAT 1
+#endif
+#define CT_CLOSED 0x80000000u  // stashed tag word: the door on the cell is closed (tags stay below bit 16)
+__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
 // MAXPTS == 0 (LR): the long-ray render (rays of 65..255 points, k_obs_lr): each ray is walked in 32-point segments
 // from the 16-bit ray table, and the per-agent tables (first-visit table, wall suppression, sinks, dirt bitmap,
 // agent masks, dirt map, packed queue) live in the wave's HBM pool slot `slot` instead of LDS.
@@ -2532,6 +2541,9 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   // packed mode: queue of the agent row's nonzero entries awaiting the fused projection ([64] flat index, [64] value);
   // the weight rows of up to 4 entries are loaded together, so their L2 latencies overlap instead of chaining
   tu32* pq = wdirt + (DIRT ? dd : 0);
+  // dense obs (FLAT): per window cell the stashed tag word (placement, then the flattened store pass)
+  constexpr bool FLAT = PK == 0 && MFG_OBS_FLAT;
+  tu32* ctag = pq + 2 * MFG_WAVE;
   constexpr bool has_dirt = DIRT;  // S->dirt_cap != 0 (a template parameter: the register budget of k_obs)
   const float invW = 1.0f / (float)W;
   // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
@@ -2868,6 +2880,13 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         if (tag == MFG_TAG_MACHINES) return (double)S->s.machine_pause;  // idle forever: encoding 15 (Q18)
         return 1.0;
       };
+      if constexpr (FLAT) {  // stash: the flattened pass below writes the layers (each lane only its own cell here)
+        ctag[wi] = tags | ((m & CM_DCLOSED) ? CT_CLOSED : 0u);
+        amw[2 * wi] = (uint32_t)amask;
+        amw[2 * wi + 1] = (uint32_t)(amask >> 32);
+        if (has_dirt) wdirt[wi] = v ? wdirt[wi] : 0u;
+        continue;
+      }
       OT* op = PK ? nullptr : out_a + wi;  // this lane's cell of layer l: op + l * dd (advanced per layer)
       for (int l = 0; l < nl; l++, op += PK ? 0 : dd) {
         const uint32_t tf = (uint32_t)rl((int)lr_tf, l);
@@ -2940,6 +2959,63 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         } else {
           if (inwin) __builtin_nontemporal_store(out, op);
         }
+#endif
+      }
+    }
+    if constexpr (FLAT) {
+      // the agent's [nl][dd] block as consecutive runs of 64 values: lane = element el = l * dd + c (l, c by a float
+      // reciprocal, exact for el < 2^22), the cell's stashed words from LDS, the layer record of layer l from lane l
+      // (ds_bpermute); the value formulas are the per-layer placement's. Lanes past the block repeat its last value.
+      tbl_sync<LR>();
+      const int ne = nl * dd;
+      const float invdd = 1.0f / (float)dd;
+      for (int e0 = 0; e0 < ne; e0 += MFG_WAVE) {
+        const int el = min(e0 + lane, ne - 1);
+        const int l = (int)(((float)el + 0.5f) * invdd), c = el - l * dd;
+        const uint32_t ct = ctag[c];
+        const u64 am = (u64)amw[2 * c] | ((u64)amw[2 * c + 1] << 32);
+        const uint32_t tf = bperm(l, lr_tf);
+        const uint64_t ab = (uint64_t)bperm(l, lr_alo) | ((uint64_t)bperm(l, lr_ahi) << 32);
+        const uint32_t ut = tf & 0xFFFFu, fl = tf >> 16;
+        OT out = (OT)(popc(ct & ut) + popc(am & ab));  // a small count: exact in OT
+        if (fl) {
+          auto tagv = [&](int tag) -> double {
+            if (tag >= MFG_TAG_AGENT0) return ((am >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
+            if (!((ct >> tag) & 1u)) return 0.0;
+            if (tag == MFG_TAG_DOORS) return (ct & CT_CLOSED) ? 0.6666 : 0.4444;
+            if (tag == MFG_TAG_DIRT) {
+              const uint32_t di = has_dirt ? (uint32_t)wdirt[c] : 0u;
+              return di ? e.dirtamt()[di - 1] : 0.0;
+            }
+            if (tag == MFG_TAG_MACHINES) return (double)S->s.machine_pause;  // idle forever: encoding 15 (Q18)
+            return 1.0;
+          };
+          double val = 0.0;
+          if (fl & LR_DOOR) {
+            val = tagv(MFG_TAG_DOORS);
+          } else if (fl & LR_DIRT) {
+            val = tagv(MFG_TAG_DIRT);
+          } else if (fl & LR_MACHINE) {
+            val = tagv(MFG_TAG_MACHINES);
+          } else if (fl & LR_ORDERED) {
+            const int nc = S->s.combined_n[a];
+            for (int q = 0; q < nc; q++) {
+              const double tv = tagv(S->s.combined_tags[a][q]);
+              val = q == 0 ? tv : val + tv;
+            }
+          } else if (fl & LR_BATTERY) {
+            val = c == 0 ? (frozen ? e.fbat()[a] : e.bat()[a]) : 0.0;
+          } else {  // LR_GLOBALPOS
+            const int gp = frozen ? e.fgp()[a] : apos;
+            val = c == 0 ? (double)(gp / W) / (double)H : (c == 1 ? (double)(gp % W) / (double)W : 0.0);
+          }
+          out = (OT)val;
+        }
+#if defined(MFG_ABLATE_OB_NOSTORE)
+        if (out == (OT)-12345.0) out_a[el] = out;
+#else
+        if constexpr (MW && MAXPTS <= MFG_OBS_PLAIN_PTS) out_a[el] = out;
+        else __builtin_nontemporal_store(out, out_a + el);
 #endif
       }
     }
