@@ -62,6 +62,9 @@ def lib():
         L.oracle_mt_u32_seq.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         L.oracle_mt_shuffle_range.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_pcg_seq.argtypes = [C.c_uint32, C.c_int, C.c_void_p, C.c_void_p, C.c_double, C.c_double]
+        L.oracle_rollout.argtypes = [C.c_void_p, C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_uint32, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_rollout.restype = C.c_int
         _lib = L
     return _lib
 
@@ -207,3 +210,30 @@ def pcg_seq(seed, n, lo, hi):
     uni = np.zeros(n, np.float64)
     lib().oracle_pcg_seq(seed, n, _p(raw), _p(uni), lo, hi)
     return raw, uni
+
+
+def rollout(spec, seed_base, first, n_envs, n_steps, philox_seed, threads=16):
+    """Envs first .. first + n_envs - 1 (seeded seed_base + env), reset, then n_steps of the engine's synthetic
+    actions with auto-reset, no obs (oracle_rollout, the C loop; blocks of envs run in threads: ctypes releases the
+    GIL). Returns per env: f64 reward sums [n, A], episode ends [n], final MT state + index [n, 625], floor order
+    [n, n_floor]. Test helper (tests/test_gpu_timed_path.py)."""
+    from concurrent.futures import ThreadPoolExecutor
+    L = lib()
+    A, nf = spec.n_agents, spec.c.n_floor
+    rew = np.zeros((n_envs, A), np.float64)
+    nd = np.zeros(n_envs, np.int32)
+    mt = np.zeros((n_envs, 625), np.uint32)
+    fl = np.zeros((n_envs, nf), np.int32)
+    bounds = np.linspace(0, n_envs, max(1, min(threads, n_envs)) + 1).astype(np.int64)
+
+    def run(k):
+        a, b = int(bounds[k]), int(bounds[k + 1])
+        if b <= a:
+            return 0
+        return L.oracle_rollout(C.byref(spec.c), seed_base, first + a, b - a, n_steps, philox_seed,
+                                _p(rew[a:]), _p(nd[a:]), _p(mt[a:]), _p(fl[a:]))
+    with ThreadPoolExecutor(len(bounds) - 1) as ex:
+        rcs = list(ex.map(run, range(len(bounds) - 1)))
+    if any(rcs):
+        raise RuntimeError('oracle_rollout failed')
+    return rew, nd, mt, fl

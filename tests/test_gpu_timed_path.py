@@ -118,6 +118,50 @@ def _timed_path(odt):
     assert step > 500 and ndone == len(idx)  # every sampled env crossed the step-500 episode boundary
 
 
+@pytest.mark.timeout(900)
+def test_timed_path_k8_b65536_final_state_of_16384_envs(full=False):
+    """the benched mode (K = 8, Philox actions, f64 obs, auto-reset, B = 65,536, 608 steps across the
+    step-500 mass reset, where every env goes through the done list at once) checked against the C oracle's own rollout
+    of the same envs (oracle/oracle.py rollout: the C loop, blocks in threads) on 16,384 envs (16 blocks of 1,024 spread
+    over the batch, env 0 and B - 1 included; full=True: every env, ~40M oracle env-steps, 165 s on the test box,
+    profiles/r05m_final_state_all_65536_envs.txt): per env the f64 reward sum of every agent (added step by step on both
+    sides, so ==), the number of episode ends, and the final MT19937 state, index and floor order. (The per-step obs,
+    rewards and events of 256 of these envs are compared in the tests above.) The default keeps the test well under a
+    minute: the harness takes a command silent for 3 minutes as hung."""
+    import oracle as O
+    B, K, calls, pseed = 65536, 8, 76, 12345
+    torch, spec, eng = _engine('large8.yaml', B)
+    buf = _buffers(torch, eng, K, torch.float64)
+    eng.reset(obs=buf['obs'][0], init=True, seed_base=0)
+    rsum = torch.zeros((B, spec.n_agents), dtype=torch.float64, device=eng.device)
+    ndone = torch.zeros(B, dtype=torch.int32, device=eng.device)
+    for c in range(calls):
+        eng.step(K, actions=None, philox_seed=pseed, env_base=0, step_base=c * K, auto_reset=True, **buf)
+        for k in range(K):  # the oracle adds step by step: the same f64 additions in the same order
+            rsum += buf['reward'][k]
+            ndone += buf['done'][k].to(torch.int32)
+    st = eng.export_state().cpu().numpy()
+    rs, nd = rsum.cpu().numpy(), ndone.cpu().numpy()
+    eng.close()
+    lay, nf = eng.layout, spec.c.n_floor
+    blocks = [(k * 4096, 4096) for k in range(B // 4096)] if full else \
+        [(k * 4096 + (3072 if k == 15 else 0), 1024) for k in range(B // 4096)]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(len(blocks)) as ex:
+        res = list(ex.map(lambda b: O.rollout(spec, 0, b[0], b[1], calls * K, pseed, threads=1), blocks))
+    for (s0, n), (rw, dn, mt, fl) in zip(blocks, res):
+        sl = slice(s0, s0 + n)
+        rec = st[sl]
+        g_mt = rec[:, lay['o_mt']:lay['o_mt'] + 4 * 624].copy().view(np.uint32)
+        g_idx = rec[:, lay['o_hdr']:lay['o_hdr'] + 160].copy().view(np.int32)[:, 6]  # H_MT_IDX
+        g_fl = rec[:, lay['o_perm']:lay['o_perm'] + 2 * nf].copy().view(np.uint16).astype(np.int32)
+        bad = np.nonzero((rs[sl] != rw).any(1) | (nd[sl] != dn) | (g_mt != mt[:, :624]).any(1) |
+                         (g_idx != mt[:, 624].astype(np.int32)) | (g_fl != fl).any(1))[0]
+        assert not len(bad), f'{len(bad)} envs differ from the oracle, first env {s0 + int(bad[0])}'
+        assert (dn >= 1).all()  # every checked env crossed the step-500 episode boundary
+    assert sum(n for _, n in blocks) == (B if full else B // 4)
+
+
 @pytest.mark.parametrize('cfg,B,steps', [('large8.yaml', 4096, 80), ('rooms4.yaml', 2048, 120),
                                          ('maint_rooms.yaml', 256, 96), ('alltest16.yaml', 512, 64)])
 def test_fused_k8_equals_k1(cfg, B, steps):
