@@ -369,6 +369,9 @@ def main():
     ap.add_argument('--rank-timeout', type=float, default=900.0,
                     help='bench.py --gpus N as its own launcher: kill the ranks after this many seconds')
     ap.add_argument('--no-profile', action='store_true', help='no per-kernel HIP events in the timed region')
+    ap.add_argument('--serial', action='store_true',
+                    help='attribution run: every kernel on one stream (mfg_variant.serial), so per-kernel times '
+                         'exclude the second stream\'s overlap (C4); not a headline line')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU rehearsal of the rank protocol (gloo, no GPU, no engine); not a bench number')
     args = ap.parse_args()
@@ -389,7 +392,7 @@ def main():
     spec = compile_spec(args.config)
     B, A, F = args.batch, spec.n_agents, args.fuse
     dev = torch.device('cuda', local)
-    eng = Engine(spec, B, device=local)
+    eng = Engine(spec, B, device=local, variant={'serial': 1} if args.serial else None)
     env_base, _ = env_range(rank, world, B)
     obs_t = torch.float64 if args.obs_dtype == 'f64' else torch.float32
     obs = torch.zeros((F,) + eng.obs_shape(), dtype=obs_t, device=dev)
@@ -653,6 +656,7 @@ def main():
                        "envs_per_gpu": B, "global_batch": B * world,
                        "obs": f"dense {args.obs_dtype} per env-step ({obs_bytes} B)",
                        "fuse": F, "auto_reset": True, "parallelism": f"env-shard x{world}",
+                       **({"serial": "attribution run: one stream, no reset/replay overlap"} if args.serial else {}),
                        "window": f"steps {args.warmup}..{args.warmup + args.steps} of every env" + (
                            "" if args.warmup + args.steps > 500 or args.config != 'large8.yaml' else
                            " (inside the first 500-step episode: no reset and no episode-2 obs path timed; the "
@@ -662,7 +666,9 @@ def main():
                        "timed_mode_test": PARITY_TESTS[args.obs_dtype] if args.config == 'large8.yaml' else None,
                        "timed_mode": "K=8 mfg_step calls, Philox actions, auto-reset, B=65,536, 608 steps across the "
                                      "episode-500 reset; 256 envs vs their own oracle env every step (f64 rewards ==, "
-                                     "done, events, obs bits), MT19937 + floor order after every call",
+                                     "done, events, obs bits), MT19937 + floor order after every call; every env of "
+                                     "a quarter of the batch (all 65,536 in profiles/r05m_final_state_all_65536_envs"
+                                     ".txt) vs the oracle's rollout: reward sums, episode ends, final MT + floor order",
                        "fixture_seeds": "tests/golden/large8_s{0,1}: reference step replayed through the C-ABI "
                                         "(tests/test_gpu_parity.py), py_seed 0 and 1",
                        "side_lines": {"alt_obs_dtype": PARITY_TESTS['f32' if args.obs_dtype == 'f64' else 'f64'],

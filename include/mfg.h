@@ -278,6 +278,8 @@ typedef struct mfg_variant {
   int32_t pairs_lds;          /* > 0: at most this many identifier pairs in LDS, the rest in the HBM spill */
   int32_t render_slots;       /* > 0: at most this many resident waves in the long-ray render (k_obs_lr), so each
                                  strides over several envs */
+  int32_t serial;             /* 1: every kernel on the caller's stream in launch order (no resets or replay on the
+                                 engine's second stream beside the render): per-kernel times for attribution */
 } mfg_variant;
 int mfg_create_variant(const mfg_spec* spec, int device, int64_t n_envs, const mfg_variant* variant,
                        mfg_engine** out);

@@ -329,7 +329,7 @@ extern "C" int mfg_create_variant(const mfg_spec* s, int device, int64_t n_envs,
   if (!s || !out) return fail("null argument");
   if (n_envs < 1) return fail("n_envs must be >= 1");
   if (validate_spec(s)) return -1;
-  const mfg_variant none{0, 0, 0, 0, 0};
+  const mfg_variant none{0, 0, 0, 0, 0, 0};
   DevGuard g(device);
   return create_impl(s, device, n_envs, v ? *v : none, out);
 }
@@ -708,7 +708,8 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
 #endif
     e->replay2 = h.xchg_ordered && (size_t)h.lds_replay_per_wave + RP2_RING <= MFG_LDS_MAX &&
                  (MFG_REPLAY2 == 2 || (MFG_REPLAY2 == 1 && MFG_LDS_MAX / (size_t)h.lds_replay_per_wave <= 8));
-    e->overlap = MFG_RESET_OVERLAP == 2 || (MFG_RESET_OVERLAP == 1 && (long long)h.A * h.nf >= 16384);
+    e->overlap = !v.serial &&  // mfg_variant.serial: one stream, for per-kernel attribution
+                 (MFG_RESET_OVERLAP == 2 || (MFG_RESET_OVERLAP == 1 && (long long)h.A * h.nf >= 16384));
     // with long resets (overlap) and a rule that consumes the floor order inside a step, the envs that finish
     // or respawn dirt would otherwise pay up to K steps of debt on the critical path (C4: 6.7 -> 7.4M env-steps/s)
     e->replay_each = e->overlap && h.step_rng;

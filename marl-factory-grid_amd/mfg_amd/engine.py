@@ -102,7 +102,8 @@ def _check(rc, what, h=None):
 class MfgVariant(C.Structure):
     """include/mfg.h mfg_variant: exact alternative code paths forced for the parity tests."""
     _fields_ = [('shuffle_table_path', C.c_int32), ('full_temper', C.c_int32), ('bfs_hbm', C.c_int32),
-                ('pairs_lds', C.c_int32), ('render_slots', C.c_int32)]
+                ('pairs_lds', C.c_int32), ('render_slots', C.c_int32),
+                ('serial', C.c_int32)]
 
 
 class Engine:

@@ -13,4 +13,5 @@ run() {  # name, timeout, args...
 run c3 300 --steps 400 --warmup 100 --alt-steps 0 --packed-steps 0 &&
 run c2 200 --config rooms4.yaml --batch 4096 --steps 400 --warmup 100 --alt-steps 0 --packed-steps 0 &&
 run c4 300 --config alltest16.yaml --batch 32768 --steps 200 --warmup 50 --alt-steps 0 --packed-steps 0 &&
+run c4_serial 300 --config alltest16.yaml --batch 32768 --steps 200 --warmup 50 --alt-steps 0 --packed-steps 0 --serial &&
 run c5 500 --config grid128_64.yaml --batch 131072 --fuse 1 --steps 10 --warmup 3 --alt-steps 0 --packed-steps 0
