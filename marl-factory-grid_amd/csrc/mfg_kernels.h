@@ -2471,6 +2471,9 @@ struct ObsPacked {
 // [nl][dd] block as consecutive 64-value runs (lane = element) instead of one partial run per layer (0: per layer)
 #define MFG_OBS_FLAT 1
 #endif
+#ifndef MFG_OBS_FLAT_PK
+#define MFG_OBS_FLAT_PK 1  // packed renders with wide windows queue their entries from the flattened pass too
+#endif
 #define CT_CLOSED 0x80000000u  // stashed tag word: the door on the cell is closed (tags stay below bit 16)
 __device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
@@ -2541,8 +2544,12 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   // packed mode: queue of the agent row's nonzero entries awaiting the fused projection ([64] flat index, [64] value);
   // the weight rows of up to 4 entries are loaded together, so their L2 latencies overlap instead of chaining
   tu32* pq = wdirt + (DIRT ? dd : 0);
-  // dense obs (FLAT): per window cell the stashed tag word (placement, then the flattened store pass)
-  constexpr bool FLAT = PK == 0 && MFG_OBS_FLAT;
+  // FLAT: per window cell the stashed tag word (placement, then the flattened pass that stores the dense block or
+  // queues the packed entries)
+  // (packed: from windows wider than a wave on, pomdp_r >= 4 / rays of >= 10 points, where a layer's per-layer ballots
+  // cover a partial second block: C4 fused projection 8.9 -> 10.5M env-steps/s; C3's 49-cell windows stay per layer,
+  // 34.97 vs 34.3M flattened, profiles/r05_packed_flat_ab.json)
+  constexpr bool FLAT = MFG_OBS_FLAT && (PK == 0 || (MFG_OBS_FLAT_PK && (LR || MAXPTS > 8)));
   tu32* ctag = pq + 2 * MFG_WAVE;
   constexpr bool has_dirt = DIRT;  // S->dirt_cap != 0 (a template parameter: the register budget of k_obs)
   const float invW = 1.0f / (float)W;
@@ -2777,7 +2784,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     // packed mode: entry count so far and the projection accumulators (lane j holds outputs j, 64 + j, ...)
     int qbase = 0, nq = 0;  // entries flushed so far; entries in the queue
     float acc[MFG_MAX_EMB / MFG_WAVE];
-    // flush the queued entries (in (block, layer, cell) order): the stored row slots qbase + t < cap (one
+    // flush the queued entries (in flat index order with FLAT, else (block, layer, cell) order): the stored row slots qbase + t < cap (one
     // coalesced store per array instead of one partial store per layer block), then the projection
     // acc[j] += val_t * wt[idx_t][j]
     auto flush = [&]() {
@@ -2820,10 +2827,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     if (0)
 #endif
     for (int w0 = 0; w0 < dd; w0 += MFG_WAVE) {
-      // dense: lanes past the window repeat the last window cell (its value, to its address), so the layer
-      // stores need no exec mask; packed mode keeps them out (its ballots count entries)
-      const int wi = PK ? w0 + lane : min(w0 + lane, dd - 1);
-      const bool inwin = PK ? wi < dd : true;
+      // dense (and FLAT): lanes past the window repeat the last window cell (its value, to its address), so the layer
+      // stores need no exec mask; the per-layer packed placement keeps them out (its ballots count entries)
+      const int wi = PK && !FLAT ? w0 + lane : min(w0 + lane, dd - 1);
+      const bool inwin = PK && !FLAT ? wi < dd : true;
       // wi / d and wi % d through a float reciprocal (exact: (wi + 0.5) / d is >= 0.5 / d away from an integer
       // and the product's error is <= (wi + 0.5) / d * 2^-23, below that for wi < 2^22); the tests below are branch-free, every LDS
       // read has a valid clamped address and its result is masked
@@ -2966,6 +2973,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // the agent's [nl][dd] block as consecutive runs of 64 values: lane = element el = l * dd + c (l, c by a float
       // reciprocal, exact for el < 2^22), the cell's stashed words from LDS, the layer record of layer l from lane l
       // (ds_bpermute); the value formulas are the per-layer placement's. Lanes past the block repeat its last value.
+      // Packed: one ballot per 64 elements queues the nonzero ones, so a row's entries come in flat index order.
       tbl_sync<LR>();
       const int ne = nl * dd;
       const float invdd = 1.0f / (float)dd;
@@ -3010,6 +3018,25 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
             val = c == 0 ? (double)(gp / W) / (double)H : (c == 1 ? (double)(gp % W) / (double)W : 0.0);
           }
           out = (OT)val;
+        }
+        if constexpr (PK) {
+          const float fv = (float)out;
+          const bool nz = e0 + lane < ne && fv != 0.0f;
+          const u64 nzm = ballot(nz);
+          if (nzm) {
+            const int nb = popc(nzm);
+            if (nq + nb > MFG_WAVE) {
+              tbl_sync<LR>();
+              flush();
+            }
+            if (nz) {
+              const int qpos = nq + mbcnt(nzm);
+              pq[qpos] = (uint32_t)el;
+              pq[MFG_WAVE + qpos] = (uint32_t)__float_as_int(fv);
+            }
+            nq += nb;
+          }
+          continue;
         }
 #if defined(MFG_ABLATE_OB_NOSTORE)
         if (out == (OT)-12345.0) out_a[el] = out;

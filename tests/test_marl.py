@@ -130,6 +130,11 @@ def _check_rows(dense_obs, po, w, b, k):
     nnz = (flat != 0).sum(-1).to(torch.int32)
     assert torch.equal(po.count[k], nnz)
     assert torch.equal(po.dense(k).reshape(B, A, -1), flat)
+    if po.idx is not None:  # ascending flat index order (include/mfg.h: every config here has h*w <= 64 or long rays)
+        ix = po.idx[k].long()
+        n = torch.clamp(po.count[k], max=po.cap).unsqueeze(-1)
+        later = torch.arange(1, po.cap, device=ix.device) < n
+        assert bool(((ix[..., 1:] > ix[..., :-1]) | ~later).all())
     if w is None:
         return
     ref = flat.double() @ w.double().t() + b.double()
@@ -166,6 +171,11 @@ def test_packed_cap_truncation_is_reported():
     packed.reset(obs=po, init=True)
     flat = obs[0].reshape(256, spec.n_agents, -1)
     assert torch.equal(po.count[0], (flat != 0).sum(-1).to(torch.int32))
+    # a truncated row keeps its first cap entries in flat index order
+    pos = torch.arange(flat.shape[-1], device=flat.device).expand_as(flat)
+    first = torch.where(flat != 0, pos, flat.shape[-1]).sort(-1).values[..., :2]
+    full = po.count[0] >= 2
+    assert torch.equal(po.idx[0].long()[full], first[full])
     # the projection covers all entries even when the stored row is truncated
     ref = flat.double() @ w.double().t() + b.double()
     assert float((po.emb[0].double() - ref).abs().max()) < 1e-3

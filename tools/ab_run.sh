@@ -10,6 +10,6 @@ for r in 1 2; do
       --warmup 200 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
     python -c "
 import json; d=json.load(open('gpurun_out/ab_$v.json'))
-print('$v', round(d['value']/1e6,2), {k: v['mean_launch_ms'] for k, v in d['roofline']['kernels'].items()})"
+print('$v', round(d['value']/1e6,2), {k: v.get('mean_launch_ms', v.get('ms_per_step')) for k, v in d['roofline']['kernels'].items()})"
   done
 done
