@@ -241,7 +241,8 @@ enum { MFG_OBS_F32 = 0, MFG_OBS_F64 = 1, MFG_OBS_PACKED = 2 };
  *   count[a]       number of nonzero entries of the dense row (may exceed cap: only cap are stored)
  *   idx/val[a][i]  the nonzero entries, i < min(count, cap): flat index l*h*w + cell and the value, in
  *                  (64-cell block, layer, cell) order, i.e. ascending idx (the dense row's own order) when
- *                  h*w <= 64 or the observation rays have more than 8 points (e.g. pomdp_r >= 4); slots >= count are
+ *                  h*w <= 64 or the observation rays have 9..12 points (pomdp_r 4 or 5) or more than 64 (the
+ *                  long-ray render); slots >= count are
  *                  written as idx 0 / val 0, so a fixed-width gather over all cap slots is exact
  *   emb[a][j]      bias[j] + sum over ALL nonzero entries of val * wt[idx][j] (f32 fma in entry order): the
  *                  reference RecurrentAC.obs_proj (networks.py:19,52) evaluated without materialising the

@@ -474,7 +474,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
               8 * h.dd +  // + per-window-cell agent masks (u64)
               (h.dirt_cap ? 4 * h.dd : 0) +  // + window dirt map
               8 * MFG_WAVE +  // + packed-mode projection queue
-              4 * h.dd;       // + stashed tag word per window cell (dense obs, MFG_OBS_FLAT)
+              (h.maxpts == 0 || h.maxpts <= MFG_OBS_FLAT_MAXPTS ? 4 * h.dd : 0);  // + stashed tag words (FLAT)
   // replay kernel slice: [hdr 32 B][MT + perm (record bytes o_mt..o_perm+2nf, 16 B aligned)][shuffle tables]
   {
     h.xchg_ordered = v.shuffle_table_path ? 0 : probe_xchg_order(device);

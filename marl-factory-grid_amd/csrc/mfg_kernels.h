@@ -2471,6 +2471,9 @@ struct ObsPacked {
 // [nl][dd] block as consecutive 64-value runs (lane = element) instead of one partial run per layer (0: per layer)
 #define MFG_OBS_FLAT 1
 #endif
+#ifndef MFG_OBS_FLAT_MAXPTS
+#define MFG_OBS_FLAT_MAXPTS 12  // renders with longer rays keep the per-layer stores (and no stashed tag table)
+#endif
 #ifndef MFG_OBS_FLAT_PK
 #define MFG_OBS_FLAT_PK 1  // packed renders with wide windows queue their entries from the flattened pass too
 #endif
@@ -2549,7 +2552,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   // (packed: from windows wider than a wave on, pomdp_r >= 4 / rays of >= 10 points, where a layer's per-layer ballots
   // cover a partial second block: C4 fused projection 8.9 -> 10.5M env-steps/s; C3's 49-cell windows stay per layer,
   // 34.97 vs 34.3M flattened, profiles/r05_packed_flat_ab.json)
-  constexpr bool FLAT = MFG_OBS_FLAT && (PK == 0 || (MFG_OBS_FLAT_PK && (LR || MAXPTS > 8)));
+  // (dense and packed: only up to MFG_OBS_FLAT_MAXPTS ray points; C5's 18-point rays with 17 x 17 windows measured
+  // k_obs 93 -> 110 ms flattened, profiles/r05_c5_flat_ab.json)
+  constexpr bool FLAT = MFG_OBS_FLAT && (LR || MAXPTS <= MFG_OBS_FLAT_MAXPTS) &&
+                        (PK == 0 || (MFG_OBS_FLAT_PK && (LR || MAXPTS > 8)));
   tu32* ctag = pq + 2 * MFG_WAVE;
   constexpr bool has_dirt = DIRT;  // S->dirt_cap != 0 (a template parameter: the register budget of k_obs)
   const float invW = 1.0f / (float)W;
@@ -3173,6 +3179,23 @@ __device__ __forceinline__ void rec_copy(uint8_t* dst, const uint8_t* src, int b
   const int n16 = bytes >> 4;
   for (int i = lane; i < n16; i += MFG_WAVE) ((uint4*)dst)[i] = ((const uint4*)src)[i];
 }
+// The step prefix [0, o_logic) without the dirt slots at or past nd (the live pile count): [0, pos + 4 nd),
+// [id, id + 4 nd), [battery, amount + 8 nd), [pcg, o_logic), each widened to 16 B. The widening and the overlaps only
+// touch dead slots, which a lean step neither reads nor writes, so they go back unchanged.
+#ifndef MFG_LOGIC_TRIM
+#define MFG_LOGIC_TRIM 1
+#endif
+__device__ __forceinline__ void prefix_copy(uint8_t* dst, const uint8_t* src, SpecP S, int nd, int lane) {
+  auto seg = [&](int b, int end) {
+    b &= ~15;
+    end = (end + 15) & ~15;
+    for (int i = b + 16 * lane; i < end; i += 16 * MFG_WAVE) *(uint4*)(dst + i) = *(const uint4*)(src + i);
+  };
+  seg(0, S->L.o_dirt_pos + 4 * nd);
+  seg(S->L.o_dirt_id, S->L.o_dirt_id + 4 * nd);
+  seg(S->L.o_battery, S->L.o_dirt_amt + 8 * nd);
+  seg(S->L.o_pcg, S->L.o_logic);
+}
 
 // creation (init=1): random.seed(py_seed), Factory.__init__ (floor list, OBSBuilder shuffle); then reset.
 // The first observation is rendered by k_obs afterwards.
@@ -3300,6 +3323,11 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   const bool one_pass = (!full || lazy) && (bytes >> 4) <= MFG_WAVE;  // (lm: full is false)
   uint4 orig = make_uint4(0, 0, 0, 0);
   if (one_pass && e.lane < (bytes >> 4)) orig = ((const uint4*)rec)[e.lane];
+  // longer lean prefixes with dirt: only the live piles' slots (C2 / C4 / C5: 256 / 128 / 384 slots of 16 B). A lean
+  // step never appends a pile (only RespawnDirt does, in the FULL instantiations), so the count it starts with bounds
+  // every slot it reads or writes.
+  const bool trim = MFG_LOGIC_TRIM && !FULL && !one_pass && S->dirt_cap;
+  const int nd0 = trim ? min(uni(((const int*)(rec + S->L.o_hdr))[H_N_DIRT]), S->dirt_cap) : 0;
   // the actions (a buffer load or Philox) while the record load is in flight
   const int A = S->A;
   int my_act = 0;
@@ -3313,6 +3341,8 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   }
   if (one_pass) {
     if (e.lane < (bytes >> 4)) ((uint4*)e.lds)[e.lane] = orig;
+  } else if (trim) {
+    prefix_copy(e.lds, rec, S, nd0, e.lane);
   } else {
     rec_copy(e.lds, rec, bytes, e.lane);
   }
@@ -3350,6 +3380,8 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
       const uint4 v = ((const uint4*)e.lds)[e.lane];
       if (v.x != orig.x || v.y != orig.y || v.z != orig.z || v.w != orig.w) ((uint4*)rec)[e.lane] = v;
     }
+  } else if (trim) {
+    prefix_copy(rec, e.lds, S, nd0, e.lane);
   } else {
     rec_copy(rec, e.lds, bytes, e.lane);
   }

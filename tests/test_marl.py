@@ -123,15 +123,20 @@ def _engine_pair(cfg, B, K, E=96, cap=64, seed_base=0, proj=True):
     return spec, dense, packed, po, w, b
 
 
-def _check_rows(dense_obs, po, w, b, k):
-    """Packed row k == dense f32 obs bit-exactly; emb == f64 GEMM within 1e-5 relative."""
+def _check_rows(dense_obs, po, w, b, k, block_order=False):
+    """Packed row k == dense f32 obs bit-exactly; emb == f64 GEMM within 1e-5 relative. Stored entries in ascending
+    flat index order, or with block_order (renders with rays of more than 12 points) in (64-cell block, layer, cell)
+    order (include/mfg.h)."""
     B, A = dense_obs.shape[:2]
     flat = dense_obs.reshape(B, A, -1)
     nnz = (flat != 0).sum(-1).to(torch.int32)
     assert torch.equal(po.count[k], nnz)
     assert torch.equal(po.dense(k).reshape(B, A, -1), flat)
-    if po.idx is not None:  # ascending flat index order (include/mfg.h: every config here has h*w <= 64 or long rays)
+    if po.idx is not None:
         ix = po.idx[k].long()
+        if block_order:
+            dd = dense_obs.shape[-2] * dense_obs.shape[-1]
+            ix = (ix % dd) // 64 * flat.shape[-1] + ix
         n = torch.clamp(po.count[k], max=po.cap).unsqueeze(-1)
         later = torch.arange(1, po.cap, device=ix.device) < n
         assert bool(((ix[..., 1:] > ix[..., :-1]) | ~later).all())
@@ -153,12 +158,12 @@ def test_packed_obs_matches_dense(cfg, B, K, proj):
     obs = torch.zeros(dense.obs_shape(K), dtype=torch.float32, device='cuda')
     dense.reset(obs=obs[0], init=True, seed_base=5)
     packed.reset(obs=po.view(0), init=True, seed_base=5)
-    _check_rows(obs[0], po, w, b, 0)
+    _check_rows(obs[0], po, w, b, 0, block_order='grid128' in cfg)
     for it in range(3):
         dense.step(K, philox_seed=9, step_base=1 + it * K, obs=obs, auto_reset=True)
         packed.step(K, philox_seed=9, step_base=1 + it * K, obs=po, auto_reset=True)
         for k in range(K):
-            _check_rows(obs[k], po, w, b, k)
+            _check_rows(obs[k], po, w, b, k, block_order='grid128' in cfg)
     dense.close()
     packed.close()
 
