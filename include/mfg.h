@@ -23,15 +23,15 @@
 extern "C" {
 #endif
 
-#define MFG_ABI_VERSION 3
+#define MFG_ABI_VERSION 4
 
 #define MFG_MAX_AGENTS 64
-#define MFG_MAX_ACTIONS 16
-#define MFG_MAX_LAYERS 32
+#define MFG_MAX_ACTIONS 32
+#define MFG_MAX_LAYERS 64  /* one lane per layer in the render */
 #define MFG_MAX_COMBINED 72
 #define MFG_MAX_RULES 32
 #define MFG_MAX_DOORS 64
-#define MFG_MAX_POSITIONS 16  /* configured spawn / destination cells per agent */
+#define MFG_MAX_POSITIONS 64  /* configured spawn / destination cells per agent */
 
 /* ---- action opcodes (reference: environment/actions.py, modules/<m>/actions.py) ---- */
 enum {

@@ -3,12 +3,12 @@ tests/test_abi.py checks sizeof() against the compiled libraries."""
 import ctypes as C
 
 MAX_AGENTS = 64
-MAX_ACTIONS = 16
-MAX_LAYERS = 32
+MAX_ACTIONS = 32
+MAX_LAYERS = 64
 MAX_COMBINED = 72
 MAX_RULES = 32
 MAX_DOORS = 64
-MAX_POSITIONS = 16
+MAX_POSITIONS = 64
 
 # action opcodes
 ACT_NOOP, ACT_MOVE, ACT_CHARGE, ACT_CLEAN, ACT_DEST, ACT_DOORUSE, ACT_ITEM, ACT_MACHINE = range(8)
@@ -33,7 +33,7 @@ LAYER_ZERO, LAYER_TAG, LAYER_COMBINED, LAYER_BATTERY, LAYER_GLOBALPOS = range(5)
 
 DEST_ANY, DEST_ALL, DEST_SIMULTANEOUS = range(3)
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 # ev_misc row (include/mfg.h MFG_EVM_*)
 EV_MISC_N = 12
 (EVM_DOOR_COLL_LO, EVM_DOOR_COLL_HI, EVM_RESPAWN_ITEMS, EVM_DIRT_SPAWN, EVM_DIRT_VALID, EVM_DEST_REACHED, EVM_FLAGS,

@@ -72,7 +72,7 @@ def test_hip_library_exports_every_declared_symbol():
     for f in funcs:
         assert hasattr(lib, f), f'{f} declared in include/*.h but not exported'
     lib.mfg_abi_version.restype = C.c_int
-    assert lib.mfg_abi_version() == 3
+    assert lib.mfg_abi_version() == 4
 
 
 def _hip_lib():
@@ -141,8 +141,8 @@ def test_create_validates_spec_without_touching_the_gpu():
     from mfg_amd.spec import compile_spec
     lib = _hip_lib()
     lib.mfg_create.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_void_p)]
-    cases = [('n_actions', lambda c: c.n_actions.__setitem__(0, 17), 'n_actions'),
-             ('n_layers', lambda c: c.n_layers.__setitem__(1, 40), 'n_layers'),
+    cases = [('n_actions', lambda c: c.n_actions.__setitem__(0, 33), 'n_actions'),
+             ('n_layers', lambda c: c.n_layers.__setitem__(1, 65), 'n_layers'),
              ('combined_n', lambda c: c.combined_n.__setitem__(0, 100), 'combined_n'),
              ('n_rules', lambda c: setattr(c, 'n_rules', 33), 'n_rules'),
              ('move arg', lambda c: setattr(c.actions[0][4], 'arg', 9), 'direction'),
@@ -194,4 +194,29 @@ def test_ray_length_limits(tmp_path, level, pomdp_r, pts_range):
         assert pts_range[0] <= pts <= pts_range[1]
     else:
         with pytest.raises(UnsupportedSpec, match='255 points'):
+            compile_spec(cfg)
+
+
+@pytest.mark.parametrize('n_agents,extra_layers,n_noop,n_pos,error', [
+    (40, 'Doors, ', 10, 20, None),            # wide40: 41 layers, 20 actions, 20 positions
+    (63, '', 24, 64, None),                   # 64 layers ('Other' of 63 agents + Walls), 32 actions, 64 positions
+    (64, 'Doors, ', 1, 1, 'too many observation layers'),
+    (4, '', 25, 1, 'too many actions'),
+    (4, '', 1, 65, 'positions')])
+def test_capacity_limits(tmp_path, n_agents, extra_layers, n_noop, n_pos, error):
+    """Round 5: up to 64 observation layers per agent (one lane per layer in the render), 32 actions and 64
+    configured spawn positions per agent; past them the spec compiler refuses cleanly."""
+    from mfg_amd.spec import compile_spec, UnsupportedSpec
+    pos = ', '.join(f"'({8 + i // 60}, {1 + i % 60})'" for i in range(n_pos))
+    acts = ', '.join(['Noop'] * n_noop + ['Move8'])
+    cfg = tmp_path / 'c.yaml'
+    cfg.write_text("General: {env_seed: 7, individual_rewards: true, level_name: large, pomdp_r: 2}\n"
+                   f"Agents: {{A: {{Actions: [{acts}], Observations: [Walls, {extra_layers}Other], "
+                   f"Positions: [{pos}], Clones: {n_agents - 1}}}}}\nEntities: {{Doors: }}\nRules: {{}}\n")
+    if error is None:
+        s = compile_spec(cfg)
+        assert s.n_agents == n_agents and max(s.n_layers) == n_agents + (1 if extra_layers else 0)
+        assert max(s.n_actions) == n_noop + 8 and len(s.agent_positions[0]) == n_pos
+    else:
+        with pytest.raises(UnsupportedSpec, match=error):
             compile_spec(cfg)
