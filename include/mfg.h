@@ -310,11 +310,15 @@ int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int 
  * ev_act / ev_watch u8 [K][B][A] and
  * ev_misc i32 [K][B][MFG_EV_MISC_N] (the info-dict event rows above).
  * An action index outside [0, n_actions[a]) crashes that env (MFG_CRASH_ACTION, done = 1).
- * auto_reset != 0: an env whose step is done is reset before its obs row is rendered, so the row is the
- * new episode's first observation. Per step the engine launches k_logic, k_resetdone (auto_reset) and
- * k_obs (obs != NULL); pending floor-shuffle debt is replayed (mfg_replay) once before returning (every step
- * on specs with long resets and an in-step floor-order consumer). Work on the engine's second stream is
- * joined back to `stream` before the call returns. */
+ * auto_reset (flags): MFG_STEP_AUTO_RESET: an env whose step is done is reset before its obs row is rendered, so
+ * the row is the new episode's first observation. Per step the engine launches k_logic, k_resetdone (auto_reset)
+ * and k_obs (obs != NULL); pending floor-shuffle debt is replayed (mfg_replay) once before returning (every step
+ * on specs with long resets and an in-step floor-order consumer). MFG_STEP_DEFER_REPLAY: that final replay is
+ * left to a later call (mfg_replay, or an mfg_step without the flag), e.g. once per learner window; results are
+ * identical (the debt is always paid before the floor order or MT state is consumed), but the records' MT state
+ * and floor order are not the reference's until it runs. Work on the engine's second stream is joined back to
+ * `stream` before the call returns. */
+enum { MFG_STEP_AUTO_RESET = 1, MFG_STEP_DEFER_REPLAY = 2 };
 int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
              int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
              uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream);

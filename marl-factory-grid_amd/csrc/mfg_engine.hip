@@ -971,6 +971,8 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
                      int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
                      uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
   if (K < 1) return fail("K must be >= 1");
+  const bool defer = (auto_reset & MFG_STEP_DEFER_REPLAY) != 0;  // the call's final replay left for a later call
+  auto_reset &= MFG_STEP_AUTO_RESET;
   if (obs && obs_dtype != MFG_OBS_F32 && obs_dtype != MFG_OBS_F64 && obs_dtype != MFG_OBS_PACKED)
     return fail("obs_dtype must be MFG_OBS_F32, MFG_OBS_F64 or MFG_OBS_PACKED");
   if (obs && obs_dtype == MFG_OBS_PACKED && check_packed(e, (const mfg_packed_obs*)obs)) return -1;
@@ -1083,7 +1085,7 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
       HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
     }
   }
-  return replay_impl(e, stream);
+  return defer ? 0 : replay_impl(e, stream);
 }
 
 // snapshots (checkpoints == fixtures): whole state buffer device<->device, B * layout.size bytes

@@ -169,11 +169,12 @@ class Engine:
                'mfg_reset', self.h)
 
     def step(self, K=1, actions=None, philox_seed=0, env_base=0, step_base=0, reward=None, done=None, obs=None,
-             ev_act=None, ev_watch=None, ev_misc=None, auto_reset=True):
+             ev_act=None, ev_watch=None, ev_misc=None, auto_reset=True, defer_replay=False):
         op, dt = self._obs_arg(obs, K)
         _check(self.L.mfg_step(self.h, int(K), _ptr(actions), int(philox_seed) & 0xFFFFFFFF, int(env_base),
                                int(step_base), _ptr(reward), _ptr(done), op, dt, _ptr(ev_act),
-                               _ptr(ev_watch), _ptr(ev_misc), int(bool(auto_reset)), self._stream()), 'mfg_step',
+                               _ptr(ev_watch), _ptr(ev_misc), int(bool(auto_reset)) | (2 if defer_replay else 0),
+                               self._stream()), 'mfg_step',
                self.h)
 
     def profile(self, enable=True):

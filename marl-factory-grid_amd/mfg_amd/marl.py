@@ -590,8 +590,9 @@ class BatchedA2C:
         else:
             a = torch.multinomial(torch.softmax(logits, -1), 1, generator=self.gen).squeeze(-1)
         self.act[t].copy_(a.view(self.B, self.A))
+        # the shuffle-debt replay once per window, at its last step (MFG_STEP_DEFER_REPLAY)
         self.f.engine.step(1, actions=self.act[t], reward=self.rew[t], done=self.done[t], obs=self.slot[t + 1],
-                           auto_reset=True, step_base=self.f.t)
+                           auto_reset=True, step_base=self.f.t, defer_replay=t + 1 < self.T)
         self.f.t += 1
         d = self.done[t].bool()
         # the next entry's inputs: last action (-1 after an episode end) and the recurrent state (zero then)

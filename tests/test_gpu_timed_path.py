@@ -185,6 +185,28 @@ def test_fused_k8_equals_k1(cfg, B, steps):
     e8.close()
 
 
+@pytest.mark.parametrize('cfg,B,steps', [('large8.yaml', 2048, 64), ('alltest16.yaml', 512, 64)])
+def test_deferred_replay_equals_per_call_replay(cfg, B, steps):
+    """MFG_STEP_DEFER_REPLAY on seven of every eight K=1 calls (the replay then runs on the eighth): every output
+    of every step and the state after each eighth call equal one K=8 call (include/mfg.h: the debt is paid before
+    anything consumes the floor order; alltest16's RespawnDirt consumes it inside a step)."""
+    torch, spec, e1 = _engine(cfg, B)
+    _, _, e8 = _engine(cfg, B)
+    b1 = _buffers(torch, e1, 1, torch.float32)
+    b8 = _buffers(torch, e8, 8, torch.float32)
+    e1.reset(obs=b1['obs'][0], init=True, seed_base=71)
+    e8.reset(obs=b8['obs'][0], init=True, seed_base=71)
+    for t0 in range(0, steps, 8):
+        e8.step(8, actions=None, philox_seed=5, step_base=t0, auto_reset=True, **b8)
+        for k in range(8):
+            e1.step(1, actions=None, philox_seed=5, step_base=t0 + k, auto_reset=True, defer_replay=k < 7, **b1)
+            for name in b1:
+                assert torch.equal(b1[name][0], b8[name][k]), f'{cfg} step {t0 + k} {name}'
+        assert torch.equal(e1.export_state(), e8.export_state()), f'{cfg} state after step {t0 + 7}'
+    e1.close()
+    e8.close()
+
+
 def test_output_rows_respect_header_widths():
     """Every output buffer sized exactly as include/mfg.h documents ([K][B][A], [K][B], [K][B][MFG_EV_MISC_N],
     [K][B][A][lmax][d][d]) followed by guard words: the engine writes every row and nothing past the end."""
