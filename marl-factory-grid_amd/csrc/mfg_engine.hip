@@ -713,9 +713,9 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     // with long resets (overlap) and a rule that consumes the floor order inside a step, the envs that finish
     // or respawn dirt would otherwise pay up to K steps of debt on the critical path (C4: 6.7 -> 7.4M env-steps/s)
 #ifndef MFG_REPLAY_EACH
-#define MFG_REPLAY_EACH 0  // 1: the per-step replay beside the render for every overlapped spec (timing variant)
+#define MFG_REPLAY_EACH 0  // 1: the per-step replay beside the render for every overlapped spec, -1: never (timing)
 #endif
-    e->replay_each = e->overlap && (h.step_rng || MFG_REPLAY_EACH);
+    e->replay_each = MFG_REPLAY_EACH >= 0 && e->overlap && (h.step_rng || MFG_REPLAY_EACH);
     // render shape: one wave per env, or (ray length >= 10) one env per workgroup of nwv waves sharing the cell
     // map, whichever keeps more waves per CU (C5: 3 single-wave slices of 49 KB fit a CU, 2 workgroups of 4)
     {

@@ -3386,7 +3386,9 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     rec_copy(rec, e.lds, bytes, e.lane);
   }
   if (lazy && rng_tail) rec_copy(rec + o_tail, e.lds + o_tail, n_tail, e.lane);
-  if constexpr (lm) rec_copy(rec + ms0, e.lds + S->L.o_logic, mlen, e.lane);
+  // (lm: only the maintainer states go back; their paths are read-only here, since a maintainer whose path is used
+  // up re-routes in the SEL 2 launch, and C5's 4 x 1,000-cell paths were most of k_logic's writes)
+  if constexpr (lm) rec_copy(rec + ms0, e.lds + S->L.o_logic, min(mlen, ((S->L.o_mpath + 15) & ~15) - ms0), e.lane);
 }
 #endif
 

@@ -565,7 +565,7 @@ class BatchedA2C:
         self.agent_ids = torch.arange(self.A, device=dev).repeat(self.B)
         self.t = 0
         self.updates = 0
-        self.episodes = torch.zeros((), dtype=torch.float64, device=dev)
+        self.episodes = torch.zeros((), dtype=torch.float64, device=dev)  # finished episodes, counted per window
         self.reward_sum = torch.zeros((), dtype=torch.float64, device=dev)
         self._started = False
 
@@ -598,11 +598,9 @@ class BatchedA2C:
         # the next entry's inputs: last action (-1 after an episode end) and the recurrent state (zero then)
         self.act_in[t + 1].copy_(torch.where(d.view(-1, 1), torch.full_like(a.view(self.B, self.A), -1),
                                              a.view(self.B, self.A)))
-        keep = (~d).repeat_interleave(self.A).view(self.N, 1, 1).to(self.ha.dtype)
-        torch.mul(out['hidden_actor'], keep, out=self.ha)
-        torch.mul(out['hidden_critic'], keep, out=self.hc)
-        self.episodes += d.sum()
-        self.reward_sum += self.rew[t].sum()
+        keep = (~d).to(self.ha.dtype).view(self.B, 1, 1)  # broadcast over the env's agents
+        torch.mul(out['hidden_actor'].view(self.B, self.A, -1), keep, out=self.ha.view(self.B, self.A, -1))
+        torch.mul(out['hidden_critic'].view(self.B, self.A, -1), keep, out=self.hc.view(self.B, self.A, -1))
         self.t += 1
         if self.t == self.T:
             self.learn()
@@ -638,6 +636,9 @@ class BatchedA2C:
         """One A2C update on the window (base_ac.py:200-225), then slide: o_T becomes o_0."""
         if self.check_cap:
             self.pobs.check()
+        # episode and reward counters once per window (two reductions instead of two per step)
+        self.episodes += self.done.sum()
+        self.reward_sum += self.rew.sum()
         if not self.graph:
             self._update()
         elif self._graph is not None:
