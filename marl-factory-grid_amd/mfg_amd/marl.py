@@ -518,7 +518,7 @@ class BatchedA2C:
 
     def __init__(self, factory, net=None, n_steps=5, gamma=0.99, entropy_coef=0.01, vf_coef=0.5, gae_coef=0.0,
                  lr=3e-4, cap=32, obs_emb_size=96, action_emb_size=16, hidden_size=64, use_agent_embedding=False,
-                 check_cap=True, generator=None, engine_emb=True, graph=False):
+                 check_cap=True, generator=None, engine_emb=True, graph=False, act_graph=False):
         from .engine import PackedObs
         self.f = factory
         eng = factory.engine
@@ -542,6 +542,10 @@ class BatchedA2C:
             use_agent_embedding=use_agent_embedding)
         self.net.to(self.dev)
         self.graph = bool(graph)
+        # act_graph: each window slot's policy step (forward, sampling, action copy) captured as a HIP graph after two
+        # eager warm-ups (not with an explicit generator: its draws stay on the eager path)
+        self.act_graph = bool(act_graph) and generator is None
+        self._act_graphs, self._act_warm = {}, {}
         self.opt = torch.optim.RMSprop(self.net.parameters(), lr=lr, eps=1e-5, capturable=self.graph)
         self._graph, self._warm = None, 0
         self.T, self.gamma, self.entropy_coef, self.vf_coef, self.gae_coef = n_steps, gamma, entropy_coef, \
@@ -561,6 +565,7 @@ class BatchedA2C:
         self.h0a = torch.zeros((N, 1, H), device=dev)  # hidden state fed at entry 0 of the window
         self.h0c = torch.zeros((N, 1, self.net.hidden_size_critic), device=dev)
         self.ha, self.hc = self.h0a.clone(), self.h0c.clone()  # persistent: updated in place (graph inputs)
+        self._ha_new, self._hc_new = self.h0a.clone(), self.h0c.clone()  # the policy step's new states (static)
         self.last_loss = torch.zeros((), device=dev)
         self.agent_ids = torch.arange(self.A, device=dev).repeat(self.B)
         self.t = 0
@@ -581,6 +586,25 @@ class BatchedA2C:
         if not self._started:
             self.reset()
         t = self.t
+        self._policy_step(t)
+        # the shuffle-debt replay once per window, at its last step (MFG_STEP_DEFER_REPLAY)
+        self.f.engine.step(1, actions=self.act[t], reward=self.rew[t], done=self.done[t], obs=self.slot[t + 1],
+                           auto_reset=True, step_base=self.f.t, defer_replay=t + 1 < self.T)
+        self.f.t += 1
+        d = self.done[t].bool()
+        # the next entry's inputs: last action (-1 after an episode end) and the recurrent state (zero then)
+        a = self.act[t].long()
+        self.act_in[t + 1].copy_(torch.where(d.view(-1, 1), torch.full_like(a, -1), a))
+        keep = (~d).to(self.ha.dtype).view(self.B, 1, 1)  # broadcast over the env's agents
+        torch.mul(self._ha_new.view(self.B, self.A, -1), keep, out=self.ha.view(self.B, self.A, -1))
+        torch.mul(self._hc_new.view(self.B, self.A, -1), keep, out=self.hc.view(self.B, self.A, -1))
+        self.t += 1
+        if self.t == self.T:
+            self.learn()
+
+    def _policy(self, t):
+        """Acting at window slot t: the policy on (o_t, a_{t-1}, h_t), an action per agent into act[t], the new
+        recurrent states into the static _ha_new / _hc_new."""
         emb = self.pobs.emb[t].view(self.N, 1, -1)
         a_in = self.act_in[t].view(self.N, 1)
         out = self.net.forward_emb(emb, a_in, self.ha, self.hc, agent_ids=self.agent_ids)
@@ -590,20 +614,30 @@ class BatchedA2C:
         else:
             a = torch.multinomial(torch.softmax(logits, -1), 1, generator=self.gen).squeeze(-1)
         self.act[t].copy_(a.view(self.B, self.A))
-        # the shuffle-debt replay once per window, at its last step (MFG_STEP_DEFER_REPLAY)
-        self.f.engine.step(1, actions=self.act[t], reward=self.rew[t], done=self.done[t], obs=self.slot[t + 1],
-                           auto_reset=True, step_base=self.f.t, defer_replay=t + 1 < self.T)
-        self.f.t += 1
-        d = self.done[t].bool()
-        # the next entry's inputs: last action (-1 after an episode end) and the recurrent state (zero then)
-        self.act_in[t + 1].copy_(torch.where(d.view(-1, 1), torch.full_like(a.view(self.B, self.A), -1),
-                                             a.view(self.B, self.A)))
-        keep = (~d).to(self.ha.dtype).view(self.B, 1, 1)  # broadcast over the env's agents
-        torch.mul(out['hidden_actor'].view(self.B, self.A, -1), keep, out=self.ha.view(self.B, self.A, -1))
-        torch.mul(out['hidden_critic'].view(self.B, self.A, -1), keep, out=self.hc.view(self.B, self.A, -1))
-        self.t += 1
-        if self.t == self.T:
-            self.learn()
+        self._ha_new.copy_(out['hidden_actor'])
+        self._hc_new.copy_(out['hidden_critic'])
+
+    def _policy_step(self, t):
+        if not self.act_graph:
+            return self._policy(t)
+        g = self._act_graphs.get(t)
+        if g is not None:
+            g.replay()
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        if self._act_warm.get(t, 0) < 2:  # eager warm-up on a side stream (lazy library state outside the capture)
+            side = torch.cuda.Stream(self.dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._policy(t)
+            cur.wait_stream(side)
+            self._act_warm[t] = self._act_warm.get(t, 0) + 1
+            return
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._policy(t)
+        self._act_graphs[t] = g
+        g.replay()  # capture records only: this step's policy runs here
 
     def window(self):
         """The window's learner inputs: packed entries [N, T+1, cap], action inputs [N, T+1], starts,

@@ -233,6 +233,26 @@ def test_batched_a2c_graph_update_matches_eager():
 
 
 @pytest.mark.gpu
+def test_batched_a2c_act_graph_replays_the_policy():
+    """act_graph=True: every window slot's policy step is a captured HIP graph after two eager warm-ups; a replay
+    computes the same recurrent states as the eager policy on the same inputs (the sampled actions draw from the
+    graph's own Philox offsets), and training runs on."""
+    from mfg_amd.factory import BatchedFactory
+    from mfg_amd.marl import BatchedA2C
+    f = BatchedFactory('large8.yaml', 256, seed_base=3)
+    tr = BatchedA2C(f, n_steps=5, check_cap=True, act_graph=True)
+    tr.train(4)
+    assert sorted(tr._act_graphs) == list(range(5))
+    tr._act_graphs[0].replay()
+    ha_g, hc_g = tr._ha_new.clone(), tr._hc_new.clone()
+    tr._policy(0)
+    assert torch.equal(ha_g, tr._ha_new) and torch.equal(hc_g, tr._hc_new)
+    assert bool(torch.isfinite(tr.train(2)))
+    assert int(tr.act.min()) >= 0 and int(tr.act.max()) < tr.n_actions
+    f.close()
+
+
+@pytest.mark.gpu
 def test_a2c_loss_from_engine_projection_matches_gather():
     """The learner's obs_proj forward taken from the render's fused output gives the embedding_bag loss and
     gradients (f32 tolerance): every window slot was rendered with the current weights."""
