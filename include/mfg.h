@@ -23,14 +23,14 @@
 extern "C" {
 #endif
 
-#define MFG_ABI_VERSION 4
+#define MFG_ABI_VERSION 5
 
-#define MFG_MAX_AGENTS 64
+#define MFG_MAX_AGENTS 128  /* agents > 64: two 64-lane passes per agent-parallel step (mfg_kernels.h NW) */
 #define MFG_MAX_ACTIONS 32
 #define MFG_MAX_LAYERS 64  /* one lane per layer in the render */
-#define MFG_MAX_COMBINED 72
+#define MFG_MAX_COMBINED 144  /* members of one Combined layer: every other agent (Other) + the entity tags */
 #define MFG_MAX_RULES 32
-#define MFG_MAX_DOORS 64
+#define MFG_MAX_DOORS 128   /* doors > 64: the same two-pass kernels (the reference large_qquad level has 65) */
 #define MFG_MAX_POSITIONS 64  /* configured spawn / destination cells per agent */
 
 /* ---- action opcodes (reference: environment/actions.py, modules/<m>/actions.py) ---- */
@@ -122,7 +122,7 @@ typedef struct mfg_spec {
   int32_t H, W;
   const uint8_t* level;          /* [H*W]: 0 floor, 1 wall, 2 door */
   int32_t n_floor;
-  const int32_t* floor_cells;    /* initial floor-list order: argwhere(level != '#') row-major (level_parser.py:467) */
+  const int32_t* floor_cells;    /* initial floor-list order: argwhere(level != '#') row-major (level_parser.py:71) */
   int32_t n_walls;
   const int32_t* wall_cells;     /* Wall u_int order (row-major argwhere '#') */
   int32_t n_doors;
@@ -178,10 +178,10 @@ typedef struct mfg_spec {
  *                        bits3..7 number of destinations this agent was credited with by the reach rule
  *                        (destinations/rules.py:34-54; TickResult entity = the agent)
  * ev_misc i32 [K][B][MFG_EV_MISC_N]: slots MFG_EVM_* below. */
-#define MFG_EV_MISC_N 12
+#define MFG_EV_MISC_N 16
 enum {
   MFG_EVM_DOOR_COLL_LO = 0,  /* doors (bit d) that received a WatchCollisions result, bits 0..31 */
-  MFG_EVM_DOOR_COLL_HI = 1,  /* ... doors 32..63 */
+  MFG_EVM_DOOR_COLL_HI = 1,  /* ... doors 32..63 (doors 64..127: MFG_EVM_DOOR_COLL_2 / _3) */
   MFG_EVM_RESPAWN_ITEMS = 2, /* RespawnItems result value, -1 = no result this step (items/rules.py:35-43) */
   MFG_EVM_DIRT_SPAWN = 3,    /* RespawnDirt result value, -1 = no result (clean_up/rules.py:49-59) */
   MFG_EVM_DIRT_VALID = 4,    /* ... and its validity */
@@ -190,8 +190,12 @@ enum {
   MFG_EVM_DONE_MASK = 7,     /* bit r: rule r produced a VALID DoneResult; bit 31: WatchCollisions done */
   MFG_EVM_STEP = 8,          /* Gamestate.curr_step after the step (the info dict's 'step') */
   MFG_EVM_EPISODE = 9,       /* resets done so far */
-  MFG_EVM_MAINT_COLL = 10,   /* maintainers (collection slot bit) that received a WatchCollisions result */
-  MFG_EVM_MAINT_BASE = 11    /* u_int of the first maintainer: names are 'Maintainer[base + slot]' */
+  MFG_EVM_MAINT_COLL = 10,   /* maintainers (collection slot bit) that received a WatchCollisions result, slots 0..31 */
+  MFG_EVM_MAINT_BASE = 11,   /* u_int of the first maintainer: names are 'Maintainer[base + slot]' */
+  MFG_EVM_DOOR_COLL_2 = 12,  /* doors 64..95 that received a WatchCollisions result */
+  MFG_EVM_DOOR_COLL_3 = 13,  /* doors 96..127 */
+  MFG_EVM_MAINT_COLL_HI = 14,/* maintainer slots 32..63 */
+  MFG_EVM_RESERVED = 15      /* 0 */
 };
 
 /* Crash reasons (reference crash paths; engine capacity). A crashed env reports done = 1. */
@@ -211,8 +215,9 @@ enum {
 typedef struct mfg_events {
   uint8_t act[MFG_MAX_AGENTS];       /* ev_act row */
   uint8_t watch[MFG_MAX_AGENTS];     /* ev_watch row */
-  uint64_t door_coll;                /* MFG_EVM_DOOR_COLL_LO | HI << 32 */
-  uint64_t maint_coll;               /* MFG_EVM_MAINT_COLL */
+  uint64_t door_coll;                /* doors 0..63: MFG_EVM_DOOR_COLL_LO | HI << 32 */
+  uint64_t door_coll_hi;             /* doors 64..127: MFG_EVM_DOOR_COLL_2 | _3 << 32 */
+  uint64_t maint_coll;               /* MFG_EVM_MAINT_COLL | MFG_EVM_MAINT_COLL_HI << 32 */
   int32_t respawn_items_value;       /* MFG_EVM_RESPAWN_ITEMS */
   int32_t dirt_spawn_value;          /* MFG_EVM_DIRT_SPAWN */
   int32_t dirt_spawn_valid;          /* MFG_EVM_DIRT_VALID */
@@ -310,7 +315,7 @@ int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int 
  * ev_act / ev_watch u8 [K][B][A] and
  * ev_misc i32 [K][B][MFG_EV_MISC_N] (the info-dict event rows above).
  * An action index outside [0, n_actions[a]) crashes that env (MFG_CRASH_ACTION, done = 1).
- * auto_reset (flags): MFG_STEP_AUTO_RESET: an env whose step is done is reset before its obs row is rendered, so
+ * flags (any other bit set: the call fails and nothing runs): MFG_STEP_AUTO_RESET: an env whose step is done is reset before its obs row is rendered, so
  * the row is the new episode's first observation. Per step the engine launches k_logic, k_resetdone (auto_reset)
  * and k_obs (obs != NULL); pending floor-shuffle debt is replayed (mfg_replay) once before returning (every step
  * on specs with long resets and an in-step floor-order consumer). MFG_STEP_DEFER_REPLAY: that final replay is
@@ -321,7 +326,7 @@ int mfg_reset(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dtype, int 
 enum { MFG_STEP_AUTO_RESET = 1, MFG_STEP_DEFER_REPLAY = 2 };
 int mfg_step(mfg_engine* e, int K, const int32_t* actions, uint32_t philox_seed, uint32_t env_base,
              int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
-             uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream);
+             uint8_t* ev_watch, int32_t* ev_misc, int flags, void* stream);
 
 /* Replay pending membership-only floor shuffles (check_pos_validity, states.py:259-270, Q3). */
 int mfg_replay(mfg_engine* e, void* stream);

@@ -56,9 +56,9 @@ static_assert(H__END <= MFG_HDR_N, "header overflow");
 #define EW_PRESENT 0x20000   // present in the global pos_dict (identifier-dedup may keep it out, Q14)
 #define EW_REACHED 0x40000   // destination reached
 #define EW_NOPOS 0xFFFF
-// destination bound to an agent (Object.bind_to, entity/object.py:140-148): bits 20..26 = agent index + 1
+// destination bound to an agent (Object.bind_to, entity/object.py:140-148): bits 20..27 = agent index + 1
 #define EW_BOUND_SHIFT 20
-#define EW_BOUND(w) ((((w) >> EW_BOUND_SHIFT) & 0x7F) - 1)
+#define EW_BOUND(w) ((((w) >> EW_BOUND_SHIFT) & 0xFF) - 1)
 // door word: bit0 open, bits 8..15 time_to_close, bit16 present in the global pos_dict
 #define DW_OPEN 1
 #define DW_TTC(w) (((w) >> 8) & 0xFF)
@@ -83,7 +83,8 @@ struct MfgLayerRec {
   uint32_t unit_tags;  // entity tags (< 16) counted as 1.0
   uint32_t flags;      // LR_*: door / dirt / machine value of a single-tag layer, regex-bound layers, or a
                        // Combined layer that needs its ordered left-to-right f64 sum (non-unit members)
-  uint64_t agent_bits; // agents counted as 1.0
+  uint64_t agent_bits; // agents 0..63 counted as 1.0
+  uint64_t agent_bits2;// agents 64..127 (specs with more than 64 agents)
 };
 
 struct MfgDevSpec {
@@ -146,6 +147,10 @@ struct MfgDevSpec {
   int32_t comb_fast[MFG_MAX_AGENTS];
   uint32_t comb_unit_tags[MFG_MAX_AGENTS];
   uint64_t comb_agents[MFG_MAX_AGENTS];
+  uint64_t comb_agents2[MFG_MAX_AGENTS];  // agents 64..127
+  // 64-lane passes of the agent- and door-parallel code: 1, or 2 when the spec has more than 64 agents or doors (the
+  // NW template parameter of k_logic / k_reset / k_resetdone; the render branches on the agent count at run time)
+  int32_t lane_passes;
   const MfgLayerRec* lrec;   // [A][lmax] layer records
   // long-ray render (maxpts == 0: rays of 65..255 points, k_obs_lr): the ray table with 16-bit offsets, and the
   // per-agent tables (first-visit table, wall suppression, sinks, dirt bitmap, agent masks, dirt map, packed queue:
@@ -154,7 +159,8 @@ struct MfgDevSpec {
   int32_t lrpts;             // points per ray slot of ray_pts16 (a multiple of 32)
   int32_t obs_slots;         // resident long-ray render waves (grid of k_obs_lr), each owning one pool slot
   int64_t obs_slot_bytes;    // bytes per slot
-  uint8_t* obs_pool;         // [obs_slots][obs_slot_bytes]
+  uint8_t* obs_pool;         // [2][obs_slots][obs_slot_bytes]: slots of the all-env render, then of the done-list
+                             // render (the two may run at the same time on the two streams of mfg_step)
   // rules that act in each step phase, in rule order (spawn rules and the like act only at reset)
   int32_t n_ph[3];                       // tick_step, tick_post_step, on_check_done
   uint8_t ph_rule[3][MFG_MAX_RULES];

@@ -95,7 +95,8 @@ extern "C" int mfg_decode_events(const uint8_t* ev_act, const uint8_t* ev_watch,
   for (int a = 0; a < n_agents; a++) { out->act[a] = ev_act[a]; out->watch[a] = ev_watch[a]; }
   const int32_t* m = ev_misc;
   out->door_coll = (uint64_t)(uint32_t)m[MFG_EVM_DOOR_COLL_LO] | ((uint64_t)(uint32_t)m[MFG_EVM_DOOR_COLL_HI] << 32);
-  out->maint_coll = (uint64_t)(uint32_t)m[MFG_EVM_MAINT_COLL];
+  out->door_coll_hi = (uint64_t)(uint32_t)m[MFG_EVM_DOOR_COLL_2] | ((uint64_t)(uint32_t)m[MFG_EVM_DOOR_COLL_3] << 32);
+  out->maint_coll = (uint64_t)(uint32_t)m[MFG_EVM_MAINT_COLL] | ((uint64_t)(uint32_t)m[MFG_EVM_MAINT_COLL_HI] << 32);
   out->respawn_items_value = m[MFG_EVM_RESPAWN_ITEMS];
   out->dirt_spawn_value = m[MFG_EVM_DIRT_SPAWN];
   out->dirt_spawn_valid = m[MFG_EVM_DIRT_VALID];
@@ -353,16 +354,18 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   h.dd = h.oh * h.ow;
   h.fr = std::min(h.oh, h.ow);
   h.nrays = s->n_rays;
+  h.lane_passes = (s->n_agents > MFG_WAVE || s->n_doors > MFG_WAVE) ? 2 : 1;
   for (int a = 0; a < s->n_agents; a++) {  // combined layers that are plain member counts (MfgDevSpec)
     uint32_t tm = 0;
-    uint64_t am = 0;
+    uint64_t am[2] = {0, 0};
     bool fast = true;
     for (int q = 0; q < s->combined_n[a]; q++) {
       const int t = s->combined_tags[a][q];
       if (t >= MFG_TAG_AGENT0) {
-        const uint64_t bit = 1ull << (t - MFG_TAG_AGENT0);
-        fast = fast && !(am & bit);
-        am |= bit;
+        const int b = t - MFG_TAG_AGENT0;
+        const uint64_t bit = 1ull << (b & 63);
+        fast = fast && !(am[b >> 6] & bit);
+        am[b >> 6] |= bit;
       } else {
         const bool unit = t != MFG_TAG_DOORS && t != MFG_TAG_DIRT && t != MFG_TAG_MACHINES;
         fast = fast && unit && !(tm & (1u << t));
@@ -371,7 +374,8 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     }
     h.comb_fast[a] = fast && s->combined_n[a] > 0;
     h.comb_unit_tags[a] = tm;
-    h.comb_agents[a] = am;
+    h.comb_agents[a] = am[0];
+    h.comb_agents2[a] = am[1];
   }
   if (h.nrays > 4 * MFG_WAVE) { delete e; return fail("more than 256 rays"); }
   {  // points per ray (<= fr + 1), rounded up to a compiled k_obs instantiation (DISPATCH_MP)
@@ -467,11 +471,11 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     h.max_pairs = std::max(16, 2 * tot_cap + 3 * tot_cap);
   }
   h.pair_pool = nullptr;
-  h.lds_logic = h.step_rng ? h.lds_full : h.L.o_logic + 4 * MFG_WAVE;  // step prefix + per-door count scratch
+  h.lds_logic = h.step_rng ? h.lds_full : h.L.o_logic + 4 * MFG_WAVE * h.lane_passes;  // step prefix + per-door count scratch
   h.fv_words = align_up((2 * h.fr + 1) * (2 * h.fr + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
-              8 * h.dd +  // + per-window-cell agent masks (u64)
+              8 * h.lane_passes * h.dd +  // + per-window-cell agent masks (u64 per 64 agents)
               (h.dirt_cap ? 4 * h.dd : 0) +  // + window dirt map
               8 * MFG_WAVE +  // + packed-mode projection queue
               (h.maxpts == 0 || h.maxpts <= MFG_OBS_FLAT_MAXPTS ? 4 * h.dd : 0);  // + stashed tag words (FLAT)
@@ -604,16 +608,21 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     for (int a = 0; a < h.A; a++)
       for (int l = 0; l < s->n_layers[a]; l++) {
         MfgLayerRec& R = lrec[(size_t)a * h.lmax + l];
-        R = MfgLayerRec{0u, 0u, 0ull};
+        R = MfgLayerRec{0u, 0u, 0ull, 0ull};
         const int kind = s->layers[a][l].kind, tag = s->layers[a][l].tag;
         if (kind == MFG_LAYER_TAG) {
-          if (tag >= MFG_TAG_AGENT0) R.agent_bits = 1ull << (tag - MFG_TAG_AGENT0);
+          if (tag >= MFG_TAG_AGENT0 + MFG_WAVE) R.agent_bits2 = 1ull << (tag - MFG_TAG_AGENT0 - MFG_WAVE);
+          else if (tag >= MFG_TAG_AGENT0) R.agent_bits = 1ull << (tag - MFG_TAG_AGENT0);
           else if (tag == MFG_TAG_DOORS) R.flags = LR_DOOR;
           else if (tag == MFG_TAG_DIRT) R.flags = LR_DIRT;
           else if (tag == MFG_TAG_MACHINES) R.flags = LR_MACHINE;
           else R.unit_tags = 1u << tag;
         } else if (kind == MFG_LAYER_COMBINED) {
-          if (h.comb_fast[a]) { R.unit_tags = h.comb_unit_tags[a]; R.agent_bits = h.comb_agents[a]; }
+          if (h.comb_fast[a]) {
+            R.unit_tags = h.comb_unit_tags[a];
+            R.agent_bits = h.comb_agents[a];
+            R.agent_bits2 = h.comb_agents2[a];
+          }
           else R.flags = LR_ORDERED;
         } else if (kind == MFG_LAYER_BATTERY) {
           R.flags = LR_BATTERY;
@@ -691,8 +700,11 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   {  // k_resetdone's grid: the waves resident at once (one round; each strides over the done list)
     const int wpb = wpb_for(h.lds_full);
     int per_cu = 0, n_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resetdone, wpb * 64, (size_t)h.lds_full * wpb) !=
-            hipSuccess ||
+    const hipError_t occ = h.lane_passes == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resetdone<2>, wpb * 64,
+                                                                                 (size_t)h.lds_full * wpb)
+                                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resetdone<1>, wpb * 64,
+                                                                                 (size_t)h.lds_full * wpb);
+    if (occ != hipSuccess ||
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
       delete e; return fail("occupancy query failed");
     }
@@ -738,7 +750,8 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     h.obs_slots = (int)std::max<long long>(1, std::min<long long>(n_envs, 4LL * e->n_cu));
     if (v.render_slots > 0) h.obs_slots = std::min(h.obs_slots, (int)v.render_slots);  // mfg_variant (tests)
     void* pool = nullptr;
-    if (hipMalloc(&pool, (size_t)h.obs_slot_bytes * (size_t)h.obs_slots) != hipSuccess) {
+    // two slot ranges: the done-list render on the second stream and the render of the other envs run concurrently
+    if (hipMalloc(&pool, (size_t)h.obs_slot_bytes * (size_t)h.obs_slots * 2) != hipSuccess) {
       delete e; return fail("long-ray render pool allocation failed");
     }
     e->d_bufs.push_back(pool);
@@ -905,8 +918,12 @@ static int reset_impl(mfg_engine* e, const uint8_t* mask, void* obs, int obs_dty
   if (obs && obs_dtype == MFG_OBS_PACKED && check_packed(e, (const mfg_packed_obs*)obs)) return -1;
   hipStream_t st = (hipStream_t)stream;
   PROF_BEGIN(e, st);
-  hipLaunchKernelGGL(k_reset, GEOM(e->h.lds_full), st, e->d_spec,
-                     e->d_state, (long long)e->B, mask, init, (unsigned long long)seed_base);
+  if (e->h.lane_passes == 2)
+    hipLaunchKernelGGL(k_reset<2>, GEOM(e->h.lds_full), st, e->d_spec, e->d_state, (long long)e->B, mask, init,
+                       (unsigned long long)seed_base);
+  else
+    hipLaunchKernelGGL(k_reset<1>, GEOM(e->h.lds_full), st, e->d_spec, e->d_state, (long long)e->B, mask, init,
+                       (unsigned long long)seed_base);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return fail(std::string("k_reset launch: ") + hipGetErrorString(err));
   PROF_END(e, st, MFG_K_RESET);
@@ -971,6 +988,7 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
                      int64_t step_base, double* reward, uint8_t* done, void* obs, int obs_dtype, uint8_t* ev_act,
                      uint8_t* ev_watch, int32_t* ev_misc, int auto_reset, void* stream) {
   if (K < 1) return fail("K must be >= 1");
+  if (auto_reset & ~(MFG_STEP_AUTO_RESET | MFG_STEP_DEFER_REPLAY)) return fail("unknown mfg_step flag bits");
   const bool defer = (auto_reset & MFG_STEP_DEFER_REPLAY) != 0;  // the call's final replay left for a later call
   auto_reset &= MFG_STEP_AUTO_RESET;
   if (obs && obs_dtype != MFG_OBS_F32 && obs_dtype != MFG_OBS_F64 && obs_dtype != MFG_OBS_PACKED)
@@ -991,48 +1009,43 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     }
     {
     PROF_BEGIN(e, st);
+    // k_logic<FULL, MAINT, SEL, NW> over every env (NW: 64-lane agent / door passes, MfgDevSpec::nw)
+#define LAUNCH_LOGIC(FULL, MAINT, SEL, LDS)                                                                        \
+  do {                                                                                                             \
+    if (e->h.lane_passes == 2)                                                                                              \
+      hipLaunchKernelGGL((k_logic<FULL, MAINT, SEL, 2>), GEOMW(LDS, logic_wpb), st, e->d_spec, e->d_state,         \
+                         (long long)e->B, act_k, philox_seed, env_base, (long long)(step_base + k), rew_k, done_k, \
+                         eva_k, evw_k, evm_k, auto_reset, e->rd_slot);                                             \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_logic<FULL, MAINT, SEL, 1>), GEOMW(LDS, logic_wpb), st, e->d_spec, e->d_state,         \
+                         (long long)e->B, act_k, philox_seed, env_base, (long long)(step_base + k), rew_k, done_k, \
+                         eva_k, evw_k, evm_k, auto_reset, e->rd_slot);                                             \
+  } while (0)
+    const int32_t* act_k = actions ? actions + kb * A : nullptr;
+    double* rew_k = reward ? reward + kb * A : nullptr;
+    uint8_t* done_k = done ? done + kb : nullptr;
+    uint8_t* eva_k = ev_act ? ev_act + kb * A : nullptr;
+    uint8_t* evw_k = ev_watch ? ev_watch + kb * A : nullptr;
+    int32_t* evm_k = ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr;
+    const int cnt_lds = 4 * MFG_WAVE * e->h.lane_passes;  // per-door count scratch after the staged prefix
     if (e->h.bfs_bytes) {
-    // maintainers: the envs where no maintainer re-routes (and no dirt spawn fires) this step run with the step
-    // prefix + maintainer state/paths staged (no MT, permutation or BFS scratch: several times the occupancy), the
-    // rest with the full record
-    const int ms0 = e->h.L.o_mstate & ~15;
-    const int lm_lds = e->h.L.o_logic + (((e->h.L.o_grank + 15) & ~15) - ms0) + 4 * MFG_WAVE;
-    hipLaunchKernelGGL((k_logic<true, true, 1>), GEOMW(lm_lds, logic_wpb), st,
-                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
-                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
-                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
-                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset, e->rd_slot);
-    hipLaunchKernelGGL((k_logic<true, true, 2>), GEOMW(e->h.lds_logic, logic_wpb), st,
-                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
-                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
-                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
-                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset, e->rd_slot);
+      // maintainers: the envs where no maintainer re-routes (and no dirt spawn fires) this step run with the step
+      // prefix + maintainer state/paths staged (no MT, permutation or BFS scratch: several times the occupancy), the
+      // rest with the full record
+      const int ms0 = e->h.L.o_mstate & ~15;
+      const int lm_lds = e->h.L.o_logic + (((e->h.L.o_grank + 15) & ~15) - ms0) + cnt_lds;
+      LAUNCH_LOGIC(true, true, 1, lm_lds);
+      LAUNCH_LOGIC(true, true, 2, e->h.lds_logic);
     } else if (e->h.step_rng) {
-    // RespawnDirt is the only in-step RNG consumer here: the envs without a spawn this step run the lean step at
-    // its occupancy, the few with one (C4 ~1/16) the full-record step
-    const int lean_lds = e->h.L.o_logic + 4 * MFG_WAVE;
-    hipLaunchKernelGGL((k_logic<false, false, 1>), GEOMW(lean_lds, logic_wpb), st,
-                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
-                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
-                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
-                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset, e->rd_slot);
-    hipLaunchKernelGGL((k_logic<true, false, 2>), GEOMW(e->h.lds_logic, logic_wpb), st,
-                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
-                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
-                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
-                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset, e->rd_slot);
+      // RespawnDirt is the only in-step RNG consumer here: the envs without a spawn this step run the lean step at
+      // its occupancy, the few with one (C4 ~1/16) the full-record step
+      const int lean_lds = e->h.L.o_logic + cnt_lds;
+      LAUNCH_LOGIC(false, false, 1, lean_lds);
+      LAUNCH_LOGIC(true, false, 2, e->h.lds_logic);
     } else {
-    hipLaunchKernelGGL((k_logic<false, false>), GEOMW(e->h.lds_logic, logic_wpb), st,
-                       e->d_spec, e->d_state, (long long)e->B, actions ? actions + kb * A : nullptr, philox_seed,
-                       env_base, (long long)(step_base + k), reward ? reward + kb * A : nullptr,
-                       done ? done + kb : nullptr, ev_act ? ev_act + kb * A : nullptr,
-                       ev_watch ? ev_watch + kb * A : nullptr, ev_misc ? ev_misc + kb * MFG_EV_MISC : nullptr,
-                       auto_reset, e->rd_slot);
+      LAUNCH_LOGIC(false, false, 0, e->h.lds_logic);
     }
+#undef LAUNCH_LOGIC
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(std::string("k_logic launch: ") + hipGetErrorString(err));
     PROF_END(e, st, MFG_K_LOGIC);
@@ -1040,9 +1053,6 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
     const int rd_cur = e->rd_slot;
     e->rd_slot ^= 1;  // the next k_logic appends to the other list (and empties this one after k_resetdone)
     void* obs_k = obs && obs_dtype != MFG_OBS_PACKED ? (void*)((uint8_t*)obs + (size_t)k * obs_row) : obs;
-#ifdef MFG_ABLATE_NOOBS
-    obs_k = nullptr;
-#endif
     // With auto-reset and obs, the done envs are reset and rendered on the engine's second stream while the
     // caller's stream renders every other env (k_logic's rd_flag tells k_obs which to leave out): a step's
     // resets are a few hundred latency-bound waves (C4: ~2.4 ms) that the full render hides.
@@ -1064,8 +1074,12 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
                          (size_t)e->h.lds_replay_per_wave, rs, e->d_spec, e->d_state, (long long)e->B, rd_cur);
       const int wpb = wpb_for(e->h.lds_full);
       const long long nwg = std::min<long long>(env_grid(e, wpb), e->rd_blocks);
-      hipLaunchKernelGGL(k_resetdone, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, rs,
-                         e->d_spec, e->d_state, (long long)e->B, rd_cur);
+      if (e->h.lane_passes == 2)
+        hipLaunchKernelGGL(k_resetdone<2>, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, rs,
+                           e->d_spec, e->d_state, (long long)e->B, rd_cur);
+      else
+        hipLaunchKernelGGL(k_resetdone<1>, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, rs,
+                           e->d_spec, e->d_state, (long long)e->B, rd_cur);
       hipError_t err = hipGetLastError();
       if (err != hipSuccess) return fail(std::string("k_resetdone launch: ") + hipGetErrorString(err));
       PROF_END(e, rs, MFG_K_RESETDONE);

@@ -18,8 +18,6 @@
 // tests force exact alternative paths through the test-only mfg_create_variant, include/mfg.h):
 //   MFG_RESET_OVERLAP      resets + their renders on a second stream beside the render (below)
 //   MFG_REPLAY2            the two-wave replay: 1 by occupancy (default), 2 always (the parity suite runs it on C2-C4)
-//   MFG_ABLATE_*           timing-only ablations, results NOT exact (tools/build_ablation.sh, tools/build_obs_variant.sh,
-//                          profiles/r04_replay_ablation.json)
 #ifndef MFG_RESET_OVERLAP
 // mfg_step with auto-reset: the resets + their renders on a second stream beside the other envs' render.
 // 0 never, 1 when the reset is long (agents x floor cells >= 16384: the per-agent floor shuffles and draws of
@@ -244,9 +242,7 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
   uint32_t ctr = perm ? (uint32_t)uni((int)e.stab[MFG_STAB_CTR]) : 0u;
   while (icur >= lo) {
     if (idx >= 624) {
-#ifndef MFG_ABLATE_NOTWIST
       mt_twist(e);
-#endif
       idx = 0;
     }
     const int lmax = 624 - idx;
@@ -264,10 +260,6 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
       r = y >> __clz(icur + 1);
       const int c = has ? icur - (int)r : -1;
       A = mbcnt(ballot(c >= 63));  // lower bound: the lanes that accept whatever precedes them
-#ifdef MFG_ABLATE_NOJACOBI
-      A = mbcnt(ballot(c >= 0));
-      if (0)
-#endif
       for (;;) {
         accm = ballot(A <= c);
         const int An = mbcnt(accm);
@@ -277,9 +269,6 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
       il = icur - A;
       acc = A <= c;
       act = has;
-#ifdef MFG_ABLATE_NOJACOBI
-      accm = ballot(acc);
-#endif
     } else {
       A = lane;
       for (;;) {
@@ -298,7 +287,6 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
     const int consumed = popc(ballot(act));
     const int nacc = popc(accm);
     if (first_j < 0 && nacc) first_j = rl((int)r, ffs64(accm));
-#ifndef MFG_ABLATE_NOSWAP
     if (perm && nacc) {
       const int i = acc ? il : icur, j = acc ? (int)r : icur;
       const int P0i = perm[i];
@@ -331,9 +319,6 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
         int pj = -1;
         u64 later = 0;
         u64 nm = ballot(cand);
-#ifdef MFG_ABLATE_NOPJ
-        nm = 0;
-#endif
         while (nm) {
           const int s2 = ffs64(nm);
           nm &= nm - 1;
@@ -355,7 +340,6 @@ __device__ int mt_randbelow_seq(const Env& e, int hi, int lo, PT* perm) {
         wave_sync();
       }
     }
-#endif
     icur -= nacc;
     idx += consumed;
   }
@@ -446,9 +430,7 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
   while (icur >= lo) {
     if (idx > 560) {
       if (idx >= 624) {
-#ifndef MFG_ABLATE_NOTWIST
         mt_twist(e);
-#endif
         idx -= 624;
       }
       const int jw = idx + lane;
@@ -474,17 +456,12 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // chunk instead of 2.15 from the sure lower bound c_l >= l, simulated over C3's chunks). Any seed converges to
     // the same unique fixed point (lane l is exact after l rounds).
     u64 m = ballot(c >= lane34);
-#ifdef MFG_ABLATE_NOJACOBI  // timing only: the seed taken as the accepted set (no fixed-point iteration)
-    const int A = mbcnt(m);
-#else
     const int A = accept_ranks(m, c);
-#endif
     const int nacc = popc(m);
     // ranks are monotone in the lane: all 64 words are consumed unless the band fills (nacc = span + 1), and then
     // exactly the lanes up to the last accepted one (scalar, no vector compare)
     const int consumed = nacc > span ? 64 - __builtin_clzll(m) : 64;
     const int inext = icur - nacc, idxn = idx + consumed;
-#ifndef MFG_ABLATE_NOSWAP
     if constexpr (!SWAP) {
       if (first_j < 0 && m) first_j = rl((int)r, ffs64(m));
       if (idxn <= 560) yw = mt[idxn + lane];
@@ -503,15 +480,6 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     // Many (small i): a rank table (tag | lane, keyed by icur - j) gives each draw its forward source
     // and pointer jumping resolves the chains.
     u64 cm = ballot(j > inext) & ballot(j < i) & m;
-#ifdef MFG_ABLATE_NOFWD
-    cm = 0;
-#endif
-#ifdef MFG_ABLATE_NOFWD_SERIAL  // timing only: chunks with few forwards skip them
-    if (popc(cm) <= RP_SERIAL_FWD) cm = 0;
-#endif
-#ifdef MFG_ABLATE_NOFWD_TABLE  // timing only: chunks with many forwards skip them
-    if (popc(cm) > RP_SERIAL_FWD) cm = 0;
-#endif
     if (cm) {
       if (popc(cm) <= RP_SERIAL_FWD) {
         const int keyv = icur - j;  // the rank whose i equals this lane's j
@@ -554,9 +522,6 @@ __device__ int replay_shuffle_t(const Env& e, uint16_t* perm, int hi) {
     if (acc) *pi = (uint16_t)F;
     wave_sync();
     }
-#else
-    if (idxn <= 560) yw = mt[idxn + lane];
-#endif
     icur = inext;
     idx = idxn;
   }
@@ -703,10 +668,6 @@ __device__ __forceinline__ void floor_shuffle(const Env& e) { floor_shuffle_t(e,
 // Pay the shuffle debt accumulated by membership-only floorlist calls (check_pos_validity, Q3).
 template <typename PT>
 __device__ void pay_debt_t(const Env& e, PT* perm) {
-#ifdef MFG_ABLATE_NODEBT
-  e.setH(H_DEBT, 0);
-  return;
-#endif
   int debt = e.H(H_DEBT);
   for (int k = 0; k < debt; k++) floor_shuffle_t(e, perm);
   e.setH(H_DEBT, 0);
@@ -802,10 +763,21 @@ __device__ __forceinline__ int grp_count(const int* tbl, int n, int cell, int ne
   for (int b = 0; b < n; b += MFG_WAVE) c += popc(grp_at(tbl + b, n - b, cell, need, lane));
   return c;
 }
-__device__ __forceinline__ u64 agents_at(const Env& e, int cell) {
+// Agent- and door-parallel code runs NW passes of 64 lanes (NW = 2: specs with more than 64 agents or doors); in pass h
+// lane l holds agent / door h * 64 + l. NW is a template parameter of the step and reset kernels
+// (MfgDevSpec::lane_passes).
+// number of agents at `cell`
+template <int NW>
+__device__ __forceinline__ int agents_count_at(const Env& e, int cell) {
   const int A = e.S->A;
-  int p = e.lane < A ? e.agpos()[e.lane] : -1;
-  return ballot(e.lane < A && p == cell);
+  int n = 0;
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int a = h * MFG_WAVE + e.lane;
+    const int p = a < A ? e.agpos()[a] : -1;
+    n += popc(ballot(a < A && p == cell));
+  }
+  return n;
 }
 __device__ __forceinline__ int door_idx(const Env& e, int cell) {
   int d = e.S->door_of[cell];
@@ -874,97 +846,54 @@ __device__ __forceinline__ bool present_closed_door(const Env& e, int cell) {
   return (w & DW_PRESENT) && !(w & DW_OPEN);
 }
 // any entity blocking the position (states.py:259-270): walls, closed doors, blocking agents
+template <int NW>
 __device__ bool blocked_at(const Env& e, int cell) {
   if (e.S->level[cell] == 1) return true;
   if (present_closed_door(e, cell)) return true;
   const int A = e.S->A;
-  bool b = e.lane < A && e.agpos()[e.lane] == cell && e.S->s.agent_blocking[e.lane];
-  return ballot(b) != 0;
+  u64 m = 0;
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int a = h * MFG_WAVE + e.lane;
+    m |= ballot(a < A && e.agpos()[a < A ? a : 0] == cell && e.S->s.agent_blocking[a < A ? a : 0]);
+  }
+  return m != 0;
 }
 // present maintainers at cell (colliders, maintenance/groups.py:11-13)
 __device__ __forceinline__ u64 maints_at(const Env& e, int cell) {
   return e.S->kmax ? grp_at(e.maints(), e.H(H_N_MAINTS), cell, EW_PRESENT, e.lane) : 0ull;
 }
 // number of colliders in the global list at cell (walls, closed doors, agents, maintainers)
+template <int NW>
 __device__ int colliders_at(const Env& e, int cell) {
   int n = (e.S->level[cell] == 1) + (present_closed_door(e, cell) ? 1 : 0);
-  return n + popc(agents_at(e, cell)) + popc(maints_at(e, cell));
-}
-// number of entities in the global list at cell (Door.tick, doors/entitites.py:109)
-__device__ int global_count(const Env& e, int cell) {
-  const int lane = e.lane;
-  int n = (e.S->level[cell] == 1);
-  int d = door_idx(e, cell);
-  if (d >= 0 && (e.door()[d] & DW_PRESENT)) n++;
-  n += popc(agents_at(e, cell));
-  n += popc(grp_at(e.items(), e.H(H_N_ITEMS), cell, EW_PRESENT, lane));
-  n += popc(grp_at(e.pods(), e.H(H_N_PODS), cell, EW_PRESENT, lane));
-  n += popc(grp_at(e.drops(), e.H(H_N_DROPS), cell, EW_PRESENT, lane));
-  n += popc(grp_at(e.dests(), e.H(H_N_DESTS), cell, EW_PRESENT, lane));
-  n += grp_count(e.dirtpos(), e.H(H_N_DIRT), cell, EW_PRESENT, lane);
-  if (e.S->mmax) n += popc(grp_at(e.machines(), e.H(H_N_MACHINES), cell, EW_PRESENT, lane));
-  n += popc(maints_at(e, cell));
-  return n;
+  return n + agents_count_at<NW>(e, cell) + popc(maints_at(e, cell));
 }
 
-// global_count for one cell per lane (each lane its own `cell`, -1 = none): the same terms as
-// global_count, counted by uniform loops over the group tables (broadcast LDS reads) instead of one
-// ballot round per cell
-__device__ int global_count_lanes(const Env& e, int cell) {
-  SpecP S = e.S;
-  const bool ok = cell >= 0;
-  const int c = ok ? cell : 0;
-  int n = ok && S->level[c] == 1;
-  const int d = ok ? door_idx(e, c) : -1;
-  if (d >= 0 && (e.door()[d] & DW_PRESENT)) n++;
-  for (int b = 0; b < S->A; b++) n += e.agpos()[b] == cell;
-  auto grp = [&](const int* tbl, int cnt) {
-    for (int i = 0; i < cnt; i++) {
-      const int w = tbl[i];
-      n += (EW_POS(w) == cell && (w & EW_PRESENT)) ? 1 : 0;
-    }
-  };
-  grp(e.items(), e.H(H_N_ITEMS));
-  grp(e.pods(), e.H(H_N_PODS));
-  grp(e.drops(), e.H(H_N_DROPS));
-  grp(e.dests(), e.H(H_N_DESTS));
-  grp(e.dirtpos(), e.H(H_N_DIRT));
-  if (S->mmax) grp(e.machines(), e.H(H_N_MACHINES));
-  if (S->kmax) grp(e.maints(), e.H(H_N_MAINTS));
-  return ok ? n : 0;
-}
-
-// colliders_at for one cell per lane (-1 = none), by uniform loops over agents and maintainers
-__device__ int colliders_lanes(const Env& e, int cell) {
-  SpecP S = e.S;
-  const bool ok = cell >= 0;
-  const int c = ok ? cell : 0;
-  int n = (ok && S->level[c] == 1) + (ok && present_closed_door(e, c) ? 1 : 0);
-  for (int b = 0; b < S->A; b++) n += e.agpos()[b] == cell;
-  const int nk = S->kmax ? e.H(H_N_MAINTS) : 0;
-  for (int i = 0; i < nk; i++) {
-    const int w = e.maints()[i];
-    n += (EW_POS(w) == cell && (w & EW_PRESENT)) ? 1 : 0;
-  }
-  return ok ? n : 0;
-}
-
-// Per door (lane = door, returned for lanes < nd): the number of entities in the global pos_dict at its cell
-// (all = global_count) or of its colliders (coll = colliders_at), by one lane-parallel LDS histogram per
-// entity table instead of a uniform loop over every table per door. cnt: >= 64 ints of LDS scratch.
-__device__ int door_cell_counts(const Env& e, int* cnt, bool coll) {
+// Per door (pass h, lane l: door h * 64 + l, counts of doors >= nd are 0): the number of entities in the global
+// pos_dict at its cell (all: Door.tick's len(pos_dict), doors/entitites.py:109) or of its colliders (coll:
+// colliders_at), by one lane-parallel LDS histogram per entity table instead of a uniform loop over every table per
+// door. cnt: >= 64 NW ints of LDS scratch.
+template <int NW>
+__device__ void door_cell_counts(const Env& e, int* cnt, bool coll, int (&out)[NW]) {
   SpecP S = e.S;
   const int lane = e.lane, nd = S->nd, HW = S->HW;
-  if (lane < nd) {
-    const int w = e.door()[lane];
-    cnt[lane] = coll ? ((w & DW_PRESENT) && !(w & DW_OPEN) ? 1 : 0) : ((w & DW_PRESENT) ? 1 : 0);
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int d = h * MFG_WAVE + lane;
+    if (d < nd) {
+      const int w = e.door()[d];
+      cnt[d] = coll ? ((w & DW_PRESENT) && !(w & DW_OPEN) ? 1 : 0) : ((w & DW_PRESENT) ? 1 : 0);
+    }
   }
   wave_sync();
   auto add = [&](int cell) {  // cell < 0 or off-grid: nothing
     const int d = ((unsigned)cell < (unsigned)HW) ? S->door_of[cell] : 0xFF;
     if (d != 0xFF) atomicAdd(&cnt[d], 1);
   };
-  if (lane < S->A) add(e.agpos()[lane]);
+#pragma unroll
+  for (int h = 0; h < NW; h++)
+    if (h * MFG_WAVE + lane < S->A) add(e.agpos()[h * MFG_WAVE + lane]);
   auto grp = [&](const int* tbl, int n) {
     for (int i = lane; i < n; i += MFG_WAVE) {
       const int w = tbl[i];
@@ -981,9 +910,9 @@ __device__ int door_cell_counts(const Env& e, int* cnt, bool coll) {
   }
   if (S->kmax) grp(e.maints(), e.H(H_N_MAINTS));
   wave_sync();
-  const int n = lane < nd ? cnt[lane] : 0;
+#pragma unroll
+  for (int h = 0; h < NW; h++) out[h] = h * MFG_WAVE + lane < nd ? cnt[h * MFG_WAVE + lane] : 0;
   wave_sync();
-  return n;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -997,30 +926,6 @@ __device__ __forceinline__ bool lane_cell_free(const Env& e, int cell) {
     if (e.agpos()[b] == cell) return false;
   const int nk = e.S->kmax ? e.H(H_N_MAINTS) : 0;
   for (int i = 0; i < nk; i++) { int w = e.maints()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
-  return true;
-}
-// a cell whose global list is empty (empty_positions)
-__device__ __forceinline__ bool lane_cell_empty(const Env& e, int cell) {
-  int d = door_idx(e, cell);
-  if (d >= 0 && (e.door()[d] & DW_PRESENT)) return false;
-  const int A = e.S->A;
-  for (int b = 0; b < A; b++)
-    if (e.agpos()[b] == cell) return false;
-  int n;
-  n = e.H(H_N_ITEMS);
-  for (int i = 0; i < n; i++) { int w = e.items()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
-  n = e.H(H_N_PODS);
-  for (int i = 0; i < n; i++) { int w = e.pods()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
-  n = e.H(H_N_DROPS);
-  for (int i = 0; i < n; i++) { int w = e.drops()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
-  n = e.H(H_N_DESTS);
-  for (int i = 0; i < n; i++) { int w = e.dests()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
-  n = e.H(H_N_DIRT);
-  for (int i = 0; i < n; i++) { int w = e.dirtpos()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
-  n = e.S->mmax ? e.H(H_N_MACHINES) : 0;
-  for (int i = 0; i < n; i++) { int w = e.machines()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
-  n = e.S->kmax ? e.H(H_N_MAINTS) : 0;
-  for (int i = 0; i < n; i++) { int w = e.maints()[i]; if (EW_POS(w) == cell && (w & EW_PRESENT)) return false; }
   return true;
 }
 // first n free cells of a fresh floor shuffle -> out[0..k) (LDS scratch), returns k
@@ -1147,20 +1052,53 @@ __device__ void dirt_delete(const Env& e, int k) {
 // ------------------------------------------------------------------------------------------------
 // step bookkeeping: rewards are accumulated per agent in the reference's result order
 // ------------------------------------------------------------------------------------------------
+template <int NW>
 struct StepOut {
-  double my_rew;      // lane a: agent a's reward sum so far
-  double g_rew;       // uniform: 'global' reward sum
-  int my_act_ev;      // lane a: act event bits
-  int my_watch_ev;    // lane a: watch event bits
-  int my_slot;        // lane a: action slot agent a executed this step, -1 if it did not act (paralyzed)
-  uint64_t door_coll;
-  uint32_t maint_coll;  // maintainers (collection slots) that received a WatchCollisions result
+  double my_rew[NW];    // pass h, lane l: agent h * 64 + l's reward sum so far
+  double g_rew;         // uniform: 'global' reward sum
+  int my_act_ev[NW];    // per agent (as my_rew): act event bits
+  int my_watch_ev[NW];  // per agent: watch event bits
+  int my_slot[NW];      // per agent: action slot it executed this step, -1 if it did not act (paralyzed)
+  u64 door_coll[NW];    // doors h * 64 + bit that received a WatchCollisions result
+  u64 maint_coll;       // maintainers (collection slots) that received a WatchCollisions result
   int respawn_items_value, dirt_spawn_value, dirt_spawn_valid, door_autoclose, done_mask, dest_reached, crashed;
   int done;
 };
 
-__device__ __forceinline__ void add_agent_reward(const Env& e, StepOut& o, int a, double r) {
-  if (e.lane == a) o.my_rew += r;
+// per-agent lane values (pass h, lane l = agent h * 64 + l): update agent a's entry (a uniform)
+template <int NW, typename T>
+__device__ __forceinline__ void agent_add(T (&v)[NW], int a, int lane, T x) {
+#pragma unroll
+  for (int h = 0; h < NW; h++)
+    if (lane + h * MFG_WAVE == a) v[h] += x;
+}
+template <int NW, typename T>
+__device__ __forceinline__ void agent_set(T (&v)[NW], int a, int lane, T x) {
+#pragma unroll
+  for (int h = 0; h < NW; h++)
+    if (lane + h * MFG_WAVE == a) v[h] = x;
+}
+// agent a's entry of a per-agent lane value (a uniform)
+template <int NW>
+__device__ __forceinline__ int agent_get(const int (&v)[NW], int a) {
+  return (NW == 1 || a < MFG_WAVE) ? rl(v[0], a & (MFG_WAVE - 1)) : rl(v[NW - 1], a & (MFG_WAVE - 1));
+}
+// bit d of a door / agent mask of NW words
+template <int NW>
+__device__ __forceinline__ void mask_set(u64 (&m)[NW], int d) {
+  if (NW == 1 || d < MFG_WAVE) m[0] |= 1ull << (d & (MFG_WAVE - 1));
+  else m[NW - 1] |= 1ull << (d & (MFG_WAVE - 1));
+}
+template <int NW>
+__device__ __forceinline__ bool mask_get(const u64 (&m)[NW], int d) {
+  return (((NW == 1 || d < MFG_WAVE) ? m[0] : m[NW - 1]) >> (d & (MFG_WAVE - 1))) & 1;
+}
+template <int NW>
+__device__ __forceinline__ bool mask_any(const u64 (&m)[NW]) {
+  u64 o = 0;
+#pragma unroll
+  for (int h = 0; h < NW; h++) o |= m[h];
+  return o != 0;
 }
 
 __device__ const CS mfg_action& action_of(const Env& e, int a, int slot) { return e.S->s.actions[a][slot]; }
@@ -1181,33 +1119,41 @@ __device__ __forceinline__ void set_agent_pos(const Env& e, int a, int cell) {
 // ------------------------------------------------------------------------------------------------
 // DoorUse.do (doors/actions.py:18-34; get_entities_near_pos, global_entities.py:13-38): toggle every door
 // present in the global pos_dict of the 3x3 around (x, y); valid if there was one
+template <int NW>
 __device__ bool door_use_at(const Env& e, int x, int y) {
   SpecP S = e.S;
   const int W = S->s.W;
   static const int MX[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
   static const int MY[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
-  u64 toggle = 0;
+  u64 toggle[NW];
+#pragma unroll
+  for (int h = 0; h < NW; h++) toggle[h] = 0;
   for (int k = 0; k < 9; k++) {
     const int px = x + MX[k], py = y + MY[k];
     if (px < 0 || py < 0 || px >= S->s.H || py >= W) continue;
     const int c = px * W + py;
     if (S->level[c] == 1) continue;
     const int d = door_idx(e, c);
-    if (d >= 0 && (e.door()[d] & DW_PRESENT)) toggle |= 1ull << d;
+    if (d >= 0 && (e.door()[d] & DW_PRESENT)) mask_set(toggle, d);
   }
-  if (!toggle) return false;
+  if (!mask_any(toggle)) return false;
   wave_sync();
-  if (e.lane < S->nd && ((toggle >> e.lane) & 1)) {
-    int w = e.door()[e.lane];
-    if (w & DW_OPEN) w &= ~DW_OPEN;
-    else w = (w & DW_PRESENT) | DW_OPEN | ((S->s.door_auto_close & 0xFF) << 8);
-    e.door()[e.lane] = w;
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int d = h * MFG_WAVE + e.lane;
+    if (d < S->nd && ((toggle[h] >> e.lane) & 1)) {
+      int w = e.door()[d];
+      if (w & DW_OPEN) w &= ~DW_OPEN;
+      else w = (w & DW_PRESENT) | DW_OPEN | ((S->s.door_auto_close & 0xFF) << 8);
+      e.door()[d] = w;
+    }
   }
   wave_sync();
   return true;
 }
 
-__device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
+template <int NW>
+__device__ void do_action(const Env& e, StepOut<NW>& o, int a, int slot) {
   SpecP S = e.S;
   const CS mfg_action& ac = action_of(e, a, slot);
   const int op = ac.op;
@@ -1222,18 +1168,18 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
     static const int DY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
     const int nx = x + DX[ac.arg], ny = y + DY[ac.arg];
     const int t = nx * W + ny;  // levels are wall-bounded: a move never leaves the grid
-    const bool blocked = blocked_at(e, t);
+    const bool blocked = blocked_at<NW>(e, t);
     int debt = 0;
     if (!blocked) debt++;  // check_pos_validity -> `pos in floorlist` shuffles (Q3)
     const bool not_blocked = !blocked && S->level[t] != 1;
     bool blocking_others = false;
-    if (S->s.agent_blocking[a]) blocking_others = colliders_at(e, t) > 0 || blocked;  // is_occupied
+    if (S->s.agent_blocking[a]) blocking_others = colliders_at<NW>(e, t) > 0 || blocked;  // is_occupied
     const bool v = pos != t && not_blocked && !blocking_others;
     if (v) {
       debt++;  // Entity.move re-checks validity (second shuffle)
       set_agent_pos(e, a, t);
       valid = 1;
-      coll = colliders_at(e, t) > 1;
+      coll = colliders_at<NW>(e, t) > 1;
     } else {
       valid = 0;
       coll = 1;
@@ -1241,7 +1187,7 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
     e.setH(H_DEBT, e.H(H_DEBT) + debt);
     wave_sync();
   } else if (op == MFG_ACT_DOORUSE) {  // doors/actions.py:18-34
-    valid = door_use_at(e, x, y);
+    valid = door_use_at<NW>(e, x, y);
   } else if (op == MFG_ACT_ITEM) {  // items/actions.py:41-63
     if (grp_at(e.drops(), e.H(H_N_DROPS), pos, EW_ALIVE, e.lane)) {
       valid = 0;  // inventories are always empty (pickup bug, Q8)
@@ -1260,7 +1206,7 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
     if (grp_at(e.pods(), e.H(H_N_PODS), pos, EW_ALIVE, e.lane)) {
       const double ch = e.bat()[a];
       if (ch >= 1.0) valid = 0;
-      else if (popc(agents_at(e, pos)) > 1) valid = 0;
+      else if (agents_count_at<NW>(e, pos) > 1) valid = 0;
       else {
         const double nv = S->s.pod_charge_rate + ch;
         wave_sync();
@@ -1290,8 +1236,8 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
     valid = 0;
   }
   const double rw = aux ? (valid ? ac.aux0 : ac.aux1) : (valid ? ac.valid_reward : ac.fail_reward);
-  add_agent_reward(e, o, a, rw);
-  if (e.lane == a) o.my_act_ev = 0x80 | (valid ? 1 : 0) | (coll ? 2 : 0) | (aux ? 4 : 0);
+  agent_add(o.my_rew, a, e.lane, rw);
+  agent_set(o.my_act_ev, a, e.lane, 0x80 | (valid ? 1 : 0) | (coll ? 2 : 0) | (aux ? 4 : 0));
 }
 
 // Agents act in list order (states.py:189-198), but most actions only depend on the agents before them
@@ -1303,131 +1249,180 @@ __device__ void do_action(const Env& e, StepOut& o, int a, int slot) {
 //   * arrival order = the running counter + the exclusive count of earlier successful movers;
 //   * floor-shuffle debt (Q3) = one per unblocked target + one per successful move, summed.
 // Each agent's own reward terms keep their order (the action result is its first term).
-__device__ int act_parallel(const Env& e, int my_act, StepOut& o) {
+// More than 64 agents (NW = 2): the run is resolved 64 agents at a time, each pass after the previous one's commit, so
+// the agents of earlier passes are at their new cells (and their door toggles applied) in the record, and the agents
+// of later passes at their old ones.
+template <int NW>
+__device__ int act_parallel(const Env& e, const int (&my_act)[NW], StepOut<NW>& o) {
   SpecP S = e.S;
   const int A = S->A, W = S->s.W, lane = e.lane;
-  const bool me = lane < A;
-  const int al = me ? lane : 0;
-  const bool par = me && e.agpar()[al] != 0;
-  const bool ok_slot = me && my_act >= 0 && my_act < S->s.n_actions[al];
-  const CS mfg_action& ac = S->s.actions[al][ok_slot ? my_act : 0];
-  const int op = ok_slot ? ac.op : -1;
-  const int pos = me ? e.agpos()[al] : -1;
-  const bool any_blocking = ballot(me && S->s.agent_blocking[al]) != 0;
-  bool simple = !me || par;
-  if (me && !par && ok_slot) {
-    if (op == MFG_ACT_NOOP || op == MFG_ACT_CHARGE || op == MFG_ACT_DOORUSE) simple = true;
-    else if (op == MFG_ACT_MOVE) simple = !any_blocking;
-    else if (op == MFG_ACT_ITEM) {
-      bool hit = false;
-      const int ni = e.H(H_N_ITEMS), ndr = e.H(H_N_DROPS);
-      for (int i = 0; i < ni; i++) { const int w = e.items()[i]; hit |= EW_POS(w) == pos && (w & EW_ALIVE); }
-      for (int i = 0; i < ndr; i++) { const int w = e.drops()[i]; hit |= EW_POS(w) == pos && (w & EW_ALIVE); }
-      simple = !hit;
-    }
+  bool any_blocking = false;
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int al = h * MFG_WAVE + lane;
+    any_blocking |= ballot(al < A && S->s.agent_blocking[al < A ? al : 0]) != 0;
   }
-  const u64 ns = ballot(!simple);
-  const int F = ns ? ffs64(ns) : A;
-  if (F == 0) return 0;
-  const bool act = me && lane < F && !par;
-  // DoorUse: the present doors in the 3x3 around the agent (doors/actions.py:18-34)
-  const int x = pos >= 0 ? pos / W : 0, y = pos >= 0 ? pos - x * W : 0;
-  u64 tm = 0;
-  if (act && op == MFG_ACT_DOORUSE) {
-    for (int k = 0; k < 9; k++) {
-      const int px = x + k / 3 - 1, py = y + k % 3 - 1;
-      if (px < 0 || py < 0 || px >= S->s.H || py >= W) continue;
-      const int c = px * W + py;
-      if (S->level[c] == 1) continue;
-      const int d = S->door_of[c];
-      if (d != 0xFF && (e.door()[d] & DW_PRESENT)) tm |= 1ull << d;
-    }
-  }
-  const u64 tm_lanes = ballot(tm != 0);
-  u64 seen = 0;  // doors toggled by DoorUse agents before this one
-  for (u64 m = tm_lanes; m; m &= m - 1) {
-    const int b = ffs64(m);
-    const u64 tb = ((u64)(uint32_t)rl((int)(uint32_t)(tm >> 32), b) << 32) | (uint32_t)rl((int)(uint32_t)tm, b);
-    if (b < lane) seen ^= tb;
-  }
-  // Move: target, blocking as this agent sees it (walls, closed present doors; states.py:240-270)
-  static const int DX[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
-  static const int DY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
-  const bool mv = act && op == MFG_ACT_MOVE;
-  const int t = mv ? pos + DX[ac.arg] * W + DY[ac.arg] : 0;  // levels are wall-bounded
-  bool blocked = false;
-  if (mv) {
-    blocked = S->level[t] == 1;
-    const int d = S->door_of[t];
-    if (!blocked && d != 0xFF) {
-      const int w = e.door()[d];
-      const bool open = ((w & DW_OPEN) != 0) ^ (((seen >> d) & 1) != 0);
-      blocked = (w & DW_PRESENT) && !open;
-    }
-  }
-  const bool vmove = mv && !blocked && t != pos;
-  const int npos = vmove ? t : pos;
-  // occupancy seen by this agent at X (its target, or its own cell for Charge)
-  const int X = mv ? t : pos;
-  int cnt = 0;
-  for (int b = 0; b < A; b++) {
-    const int nb = rl(npos, b), ob = rl(pos, b);
-    cnt += (b < lane) ? (nb == X) : ((b > lane) ? (ob == X) : 0);
-  }
-  int mcnt = 0;  // maintainers collide with a mover (colliders_at); Charge counts agents only
-  const int nk = S->kmax ? e.H(H_N_MAINTS) : 0;
-  for (int k = 0; k < nk; k++) { const int w = e.maints()[k]; mcnt += (EW_POS(w) == X && (w & EW_PRESENT)) ? 1 : 0; }
-  int valid = 0, coll = 0;
-  if (act) {
-    if (op == MFG_ACT_NOOP) valid = 1;
-    else if (op == MFG_ACT_MOVE) { valid = vmove; coll = vmove ? cnt + mcnt > 0 : 1; }
-    else if (op == MFG_ACT_DOORUSE) valid = tm != 0;
-    else if (op == MFG_ACT_CHARGE) {  // batteries/actions.py:20-31, entitites.py:98-111
-      bool pod = false;
-      const int np = e.H(H_N_PODS);
-      for (int i = 0; i < np; i++) { const int w = e.pods()[i]; pod |= EW_POS(w) == pos && (w & EW_ALIVE); }
-      const double ch = e.bat()[al];
-      if (pod && ch < 1.0 && cnt == 0) {
-        const double nv = S->s.pod_charge_rate + ch;
-        e.bat()[al] = nv > 1.0 ? 1.0 : nv;
-        valid = 1;
+  // F: the first agent outside the lane-parallel class (classified before any pass: no action of the run changes
+  // what the class depends on, the agent's own cell, slot and paralysis)
+  int F = A;
+  bool par_h[NW], ok_h[NW];
+  int pos_h[NW];
+#pragma unroll
+  for (int h = NW - 1; h >= 0; h--) {
+    const int al0 = h * MFG_WAVE + lane;
+    const bool me = al0 < A;
+    const int al = me ? al0 : 0;
+    const bool par = me && e.agpar()[al] != 0;
+    const bool ok_slot = me && my_act[h] >= 0 && my_act[h] < S->s.n_actions[al];
+    const int op = ok_slot ? S->s.actions[al][my_act[h]].op : -1;
+    const int pos = me ? e.agpos()[al] : -1;
+    par_h[h] = par;
+    ok_h[h] = ok_slot;
+    pos_h[h] = pos;
+    bool simple = !me || par;
+    if (me && !par && ok_slot) {
+      if (op == MFG_ACT_NOOP || op == MFG_ACT_CHARGE || op == MFG_ACT_DOORUSE) simple = true;
+      else if (op == MFG_ACT_MOVE) simple = !any_blocking;
+      else if (op == MFG_ACT_ITEM) {
+        bool hit = false;
+        const int ni = e.H(H_N_ITEMS), ndr = e.H(H_N_DROPS);
+        for (int i = 0; i < ni; i++) { const int w = e.items()[i]; hit |= EW_POS(w) == pos && (w & EW_ALIVE); }
+        for (int i = 0; i < ndr; i++) { const int w = e.drops()[i]; hit |= EW_POS(w) == pos && (w & EW_ALIVE); }
+        simple = !hit;
       }
-    }  // ItemAction here: no item, no drop-off on the cell -> fails
+    }
+    const u64 ns = ballot(!simple);
+    if (ns) F = h * MFG_WAVE + ffs64(ns);
   }
-  // commit: positions + arrival order, doors, debt, rewards and events
-  const u64 vm = ballot(vmove);
-  const int arr0 = e.H(H_ARRIVAL);
-  const int debt = popc(ballot(mv && !blocked)) + popc(vm);
-  wave_sync();
-  if (vmove) {
-    e.agpos()[al] = t;
-    e.agarr()[al] = arr0 + mbcnt(vm);
-  }
-  if (tm_lanes && lane < S->nd) {  // each door: the parity of its toggles; opening resets the timer
-    int n = 0;
+  if (F == 0) return 0;
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    if (h * MFG_WAVE >= F) break;
+    const int al0 = h * MFG_WAVE + lane;
+    const bool me = al0 < A;
+    const int al = me ? al0 : 0;
+    const bool par = par_h[h];
+    const bool ok_slot = ok_h[h];
+    const CS mfg_action& ac = S->s.actions[al][ok_slot ? my_act[h] : 0];
+    const int op = ok_slot ? ac.op : -1;
+    const int pos = pos_h[h];
+    const bool act = me && al0 < F && !par;
+    // DoorUse: the present doors in the 3x3 around the agent (doors/actions.py:18-34)
+    const int x = pos >= 0 ? pos / W : 0, y = pos >= 0 ? pos - x * W : 0;
+    u64 tm[NW];
+#pragma unroll
+    for (int g = 0; g < NW; g++) tm[g] = 0;
+    if (act && op == MFG_ACT_DOORUSE) {
+      for (int k = 0; k < 9; k++) {
+        const int px = x + k / 3 - 1, py = y + k % 3 - 1;
+        if (px < 0 || py < 0 || px >= S->s.H || py >= W) continue;
+        const int c = px * W + py;
+        if (S->level[c] == 1) continue;
+        const int d = S->door_of[c];
+        if (d != 0xFF && (e.door()[d] & DW_PRESENT)) mask_set(tm, d);
+      }
+    }
+    const u64 tm_lanes = ballot(mask_any(tm));
+    u64 seen[NW];  // doors toggled by DoorUse agents of this pass before this one
+#pragma unroll
+    for (int g = 0; g < NW; g++) seen[g] = 0;
     for (u64 m = tm_lanes; m; m &= m - 1) {
       const int b = ffs64(m);
-      const uint32_t lo = (uint32_t)rl((int)(uint32_t)tm, b), hi = (uint32_t)rl((int)(uint32_t)(tm >> 32), b);
-      n += ((lane < 32 ? lo : hi) >> (lane & 31)) & 1;
+#pragma unroll
+      for (int g = 0; g < NW; g++) {
+        const u64 tb = ((u64)(uint32_t)rl((int)(uint32_t)(tm[g] >> 32), b) << 32) | (uint32_t)rl((int)(uint32_t)tm[g], b);
+        if (b < lane) seen[g] ^= tb;
+      }
     }
-    if (n) {
-      const int w = e.door()[lane];
-      const bool open0 = (w & DW_OPEN) != 0;
-      const bool opened = open0 ? n >= 2 : true;
-      const bool open = open0 ^ ((n & 1) != 0);
-      e.door()[lane] = (w & DW_PRESENT) | (open ? DW_OPEN : 0) | ((opened ? (S->s.door_auto_close & 0xFF) : DW_TTC(w)) << 8);
+    // Move: target, blocking as this agent sees it (walls, closed present doors; states.py:240-270)
+    static const int DX[8] = {-1, -1, 0, 1, 1, 1, 0, -1};
+    static const int DY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+    const bool mv = act && op == MFG_ACT_MOVE;
+    const int t = mv ? pos + DX[ac.arg] * W + DY[ac.arg] : 0;  // levels are wall-bounded
+    bool blocked = false;
+    if (mv) {
+      blocked = S->level[t] == 1;
+      const int d = S->door_of[t];
+      if (!blocked && d != 0xFF) {
+        const int w = e.door()[d];
+        const bool open = ((w & DW_OPEN) != 0) ^ mask_get(seen, d);
+        blocked = (w & DW_PRESENT) && !open;
+      }
     }
+    const bool vmove = mv && !blocked && t != pos;
+    const int npos = vmove ? t : pos;
+    // occupancy seen by this agent at X (its target, or its own cell for Charge)
+    const int X = mv ? t : pos;
+    int cnt = 0;
+    const int na = min(A - h * MFG_WAVE, MFG_WAVE);
+    for (int b = 0; b < na; b++) {
+      const int nb = rl(npos, b), ob = rl(pos, b);
+      cnt += (b < lane) ? (nb == X) : ((b > lane) ? (ob == X) : 0);
+    }
+    if constexpr (NW > 1) {  // the other passes' agents from the record: earlier passes committed, later ones not yet
+      for (int b = 0; b < h * MFG_WAVE; b++) cnt += e.agpos()[b] == X;
+      for (int b = (h + 1) * MFG_WAVE; b < A; b++) cnt += e.agpos()[b] == X;
+    }
+    int mcnt = 0;  // maintainers collide with a mover (colliders_at); Charge counts agents only
+    const int nk = S->kmax ? e.H(H_N_MAINTS) : 0;
+    for (int k = 0; k < nk; k++) { const int w = e.maints()[k]; mcnt += (EW_POS(w) == X && (w & EW_PRESENT)) ? 1 : 0; }
+    int valid = 0, coll = 0;
+    if (act) {
+      if (op == MFG_ACT_NOOP) valid = 1;
+      else if (op == MFG_ACT_MOVE) { valid = vmove; coll = vmove ? cnt + mcnt > 0 : 1; }
+      else if (op == MFG_ACT_DOORUSE) valid = mask_any(tm);
+      else if (op == MFG_ACT_CHARGE) {  // batteries/actions.py:20-31, entitites.py:98-111
+        bool pod = false;
+        const int np = e.H(H_N_PODS);
+        for (int i = 0; i < np; i++) { const int w = e.pods()[i]; pod |= EW_POS(w) == pos && (w & EW_ALIVE); }
+        const double ch = e.bat()[al];
+        if (pod && ch < 1.0 && cnt == 0) {
+          const double nv = S->s.pod_charge_rate + ch;
+          e.bat()[al] = nv > 1.0 ? 1.0 : nv;
+          valid = 1;
+        }
+      }  // ItemAction here: no item, no drop-off on the cell -> fails
+    }
+    // commit: positions + arrival order, doors, debt, rewards and events
+    const u64 vm = ballot(vmove);
+    const int arr0 = e.H(H_ARRIVAL);
+    const int debt = popc(ballot(mv && !blocked)) + popc(vm);
+    wave_sync();
+    if (vmove) {
+      e.agpos()[al] = t;
+      e.agarr()[al] = arr0 + mbcnt(vm);
+    }
+    if (tm_lanes) {  // each door: the parity of its toggles; opening resets the timer
+#pragma unroll
+      for (int g = 0; g < NW; g++) {
+        const int dl = g * MFG_WAVE + lane;
+        if (dl >= S->nd) continue;
+        int n = 0;
+        for (u64 m = tm_lanes; m; m &= m - 1) {
+          const int b = ffs64(m);
+          const uint32_t lo = (uint32_t)rl((int)(uint32_t)tm[g], b), hi = (uint32_t)rl((int)(uint32_t)(tm[g] >> 32), b);
+          n += ((lane < 32 ? lo : hi) >> (lane & 31)) & 1;
+        }
+        if (n) {
+          const int w = e.door()[dl];
+          const bool open0 = (w & DW_OPEN) != 0;
+          const bool opened = open0 ? n >= 2 : true;
+          const bool open = open0 ^ ((n & 1) != 0);
+          e.door()[dl] = (w & DW_PRESENT) | (open ? DW_OPEN : 0) | ((opened ? (S->s.door_auto_close & 0xFF) : DW_TTC(w)) << 8);
+        }
+      }
+    }
+    if (lane == 0) {
+      e.hdr()[H_ARRIVAL] = arr0 + popc(vm);
+      e.hdr()[H_DEBT] += debt;
+    }
+    if (act) {
+      o.my_rew[h] += valid ? ac.valid_reward : ac.fail_reward;
+      o.my_act_ev[h] = 0x80 | (valid ? 1 : 0) | (coll ? 2 : 0);
+      o.my_slot[h] = my_act[h];
+    }
+    wave_sync();
   }
-  if (lane == 0) {
-    e.hdr()[H_ARRIVAL] = arr0 + popc(vm);
-    e.hdr()[H_DEBT] += debt;
-  }
-  if (act) {
-    o.my_rew += valid ? ac.valid_reward : ac.fail_reward;
-    o.my_act_ev = 0x80 | (valid ? 1 : 0) | (coll ? 2 : 0);
-    o.my_slot = my_act;
-  }
-  wave_sync();
   return F;
 }
 
@@ -1671,6 +1666,7 @@ __device__ void maint_move(const Env& e, int k, int cell) {
   wave_sync();
 }
 // Maintainer.tick (maintenance/entities.py:37-62); MoveMaintainers discards every result
+template <int NW>
 __device__ void maint_tick(const Env& e, int k, int* crashed) {
   SpecP S = e.S;
   const int W = S->s.W;
@@ -1726,17 +1722,17 @@ __device__ void maint_tick(const Env& e, int k, int* crashed) {
   const int nxt = uni((int)e.mpath(k)[head]);
   const int d = door_idx(e, nxt);
   if (d >= 0 && !(e.door()[d] & DW_OPEN)) {  // _closed_door_in_path -> DoorUse
-    door_use_at(e, pos / W, pos % W);
+    door_use_at<NW>(e, pos / W, pos % W);
     return;
   }
-  if (colliders_at(e, nxt) > 0) return;  // _predict_move: a collider ahead -> Noop
+  if (colliders_at<NW>(e, nxt) > 0) return;  // _predict_move: a collider ahead -> Noop
   wave_sync();
   if (e.lane == 0) st[MS_PATH_HEAD] = head + 1;
   wave_sync();
   const int dx = nxt / W - pos / W, dy = nxt % W - pos % W;
   if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || (!dx && !dy)) { *crashed = 6; return; }  // not in MOVEMAP
   // Move.do (actions.py:77-100): check_move_validity, then Entity.move re-checks (Q3: one shuffle each)
-  if (blocked_at(e, nxt)) return;
+  if (blocked_at<NW>(e, nxt)) return;
   int debt = 1;
   if (S->level[nxt] != 1) {
     debt++;
@@ -1746,26 +1742,31 @@ __device__ void maint_tick(const Env& e, int k, int* crashed) {
   wave_sync();
 }
 
-template <bool RNG, bool MAINT>
-__device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
+template <bool RNG, bool MAINT, int NW>
+__device__ void rule_tick_step(const Env& e, StepOut<NW>& o, int ri, int* scratch) {
   SpecP S = e.S;
   const CS mfg_rule& ru = S->s.rules[ri];
   const int op = ru.op;
   if (op == MFG_RULE_DOOR_AUTOCLOSE) {  // doors/rules.py:20-28, doors/entitites.py:107-122
     if (S->nd > 0) {
       const int nd = S->nd;
-      const int cnt = door_cell_counts(e, e.scratch, false);  // lane = door: len(pos_dict[door])
+      int cnt[NW];
+      door_cell_counts<NW>(e, e.scratch, false, cnt);  // per door lane: len(pos_dict[door])
       wave_sync();
-      if (e.lane < nd) {
-        int w = e.door()[e.lane];
-        if (cnt <= 2) {
-          const int ttc = DW_TTC(w);
-          if ((w & DW_OPEN) && ttc) w = (w & ~0xFF00) | ((ttc - 1) << 8);
-          else if ((w & DW_OPEN) && !ttc) w &= ~DW_OPEN;
-        } else {
-          w = (w & ~0xFF00) | ((S->s.door_auto_close & 0xFF) << 8);
+#pragma unroll
+      for (int g = 0; g < NW; g++) {
+        const int d = g * MFG_WAVE + e.lane;
+        if (d < nd) {
+          int w = e.door()[d];
+          if (cnt[g] <= 2) {
+            const int ttc = DW_TTC(w);
+            if ((w & DW_OPEN) && ttc) w = (w & ~0xFF00) | ((ttc - 1) << 8);
+            else if ((w & DW_OPEN) && !ttc) w &= ~DW_OPEN;
+          } else {
+            w = (w & ~0xFF00) | ((S->s.door_auto_close & 0xFF) << 8);
+          }
+          e.door()[d] = w;
         }
-        e.door()[e.lane] = w;
       }
       wave_sync();
       o.door_autoclose = 1;
@@ -1781,15 +1782,19 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
     }
   } else if (op == MFG_RULE_BATTERY_DECHARGE || op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:50-64
     bool missing = false;
-    if (e.lane < S->A) {
-      double cost = ru.f[0];
-      if (ru.i[2])  // per_action_costs[agent.state.identifier]: the executed action's class, 'Noop' if paralyzed
-        cost = o.my_slot >= 0 ? S->s.actions[e.lane][o.my_slot].battery_cost : (ru.i[3] ? ru.f[3] : __builtin_nan(""));
-      missing = cost != cost;
-      double b = e.bat()[e.lane];
-      if (b != 0.0 && !missing) {
-        double nv = cost + b;
-        e.bat()[e.lane] = nv > 0.0 ? nv : 0.0;
+#pragma unroll
+    for (int h = 0; h < NW; h++) {
+      const int a = h * MFG_WAVE + e.lane;
+      if (a < S->A) {
+        double cost = ru.f[0];
+        if (ru.i[2])  // per_action_costs[agent.state.identifier]: the executed action's class, 'Noop' if paralyzed
+          cost = o.my_slot[h] >= 0 ? S->s.actions[a][o.my_slot[h]].battery_cost : (ru.i[3] ? ru.f[3] : __builtin_nan(""));
+        missing |= cost != cost;
+        double b = e.bat()[a];
+        if (b != 0.0 && cost == cost) {
+          double nv = cost + b;
+          e.bat()[a] = nv > 0.0 ? nv : 0.0;
+        }
       }
     }
     if (ballot(missing)) o.crashed = MFG_CRASH_RULE;  // KeyError upstream
@@ -1814,7 +1819,7 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
   } else if (op == MFG_RULE_MOVE_MAINTAINERS) {  // maintenance/rules.py:16-21
     if constexpr (RNG && MAINT) {
       const int nk = e.H(H_N_MAINTS);
-      for (int k = 0; k < nk && !o.crashed; k++) maint_tick(e, k, &o.crashed);
+      for (int k = 0; k < nk && !o.crashed; k++) maint_tick<NW>(e, k, &o.crashed);
     } else {
       o.crashed = 1;  // unreachable: the host launches k_logic<true, true> for specs with MoveMaintainers
     }
@@ -1824,31 +1829,44 @@ __device__ void rule_tick_step(const Env& e, StepOut& o, int ri, int* scratch) {
       const int w = uni(e.dests()[i]);
       if (w & EW_REACHED) continue;
       const int cell = EW_POS(w);
-      const u64 am = agents_at(e, cell);
-      if (!am) continue;
-      const int bnd = EW_BOUND(w);  // a bound destination is reached only by its agent (rules.py:40-46)
-      if (bnd >= 0 && !((am >> bnd) & 1)) continue;
-      // the Agents-group cell list is in arrival order; the loop variable ends on the last arrival
-      int arr = e.lane < S->A && ((am >> e.lane) & 1) ? e.agarr()[e.lane] : -1;
-      int best = arr;
+      // the agents on the cell; the Agents-group cell list is in arrival order, so the loop variable ends on the
+      // last arrival
+      int best = -1;
+#pragma unroll
+      for (int h = 0; h < NW; h++) {
+        const int a = h * MFG_WAVE + e.lane;
+        const bool on = a < S->A && e.agpos()[a < S->A ? a : 0] == cell;
+        best = max(best, on ? e.agarr()[a] : -1);
+      }
       for (int o2 = 32; o2 > 0; o2 >>= 1) best = max(best, __shfl_xor(best, o2));
-      const u64 lm = ballot(arr == best && arr >= 0);
-      const int last = ffs64(lm);
+      if (best < 0) continue;  // no agent there
+      const int bnd = EW_BOUND(w);  // a bound destination is reached only by its agent (rules.py:40-46)
+      if (bnd >= 0 && uni(e.agpos()[bnd]) != cell) continue;
+      int last = -1;
+#pragma unroll
+      for (int h = NW - 1; h >= 0; h--) {
+        const int a = h * MFG_WAVE + e.lane;
+        const u64 lm = ballot(a < S->A && e.agpos()[a < S->A ? a : 0] == cell && e.agarr()[a < S->A ? a : 0] == best);
+        if (lm) last = h * MFG_WAVE + ffs64(lm);
+      }
       wave_sync();
       if (e.lane == 0) e.dests()[i] = w | EW_REACHED;
       wave_sync();
-      add_agent_reward(e, o, last, ru.f[0]);
+      agent_add(o.my_rew, last, e.lane, (double)ru.f[0]);
       // info: one '<agent>_<rule>' entry per credited destination; count per agent in ev_watch bits 3..7
-      if (e.lane == last) {
-        if (o.my_watch_ev >= (31 << 3)) e.hdr()[H_OVERFLOW] = 1;
-        else o.my_watch_ev += 1 << 3;
-      }
+#pragma unroll
+      for (int h = 0; h < NW; h++)
+        if (e.lane + h * MFG_WAVE == last) {
+          if (o.my_watch_ev[h] >= (31 << 3)) e.hdr()[H_OVERFLOW] = 1;
+          else o.my_watch_ev[h] += 1 << 3;
+        }
       o.dest_reached++;
     }
   }
 }
 
-__device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
+template <int NW>
+__device__ void rule_post_step(const Env& e, StepOut<NW>& o, int ri) {
   SpecP S = e.S;
   const CS mfg_rule& ru = S->s.rules[ri];
   const int op = ru.op;
@@ -1871,77 +1889,106 @@ __device__ void rule_post_step(const Env& e, StepOut& o, int ri) {
     const int A = S->A;
     const int nk = S->kmax ? e.H(H_N_MAINTS) : 0, mbase = S->kmax ? e.H(H_MAINT_BASE) : 0;
     bool hit = false;
-    u64 used = 0;          // int identifiers < 64 that already have a result (door indices, maintainer ids)
-    uint32_t mres = 0;     // maintainers with a result
-    bool agres = false;    // lane a: agent a has a result
+    u64 used[NW];          // int identifiers < 64 NW that already have a result (door indices, maintainer ids)
+    bool agres[NW];        // per agent: it has a result
+#pragma unroll
+    for (int h = 0; h < NW; h++) { used[h] = 0; agres[h] = false; }
+    u64 mres = 0;          // maintainers with a result
     auto maint_results = [&](int cell) {
       const u64 mk = maints_at(e, cell);
       for (u64 m = mk; m; m &= m - 1) {
         const int k = ffs64(m), id = mbase + k;
-        if ((mres >> k) & 1u) continue;
-        if (id < 64 && ((used >> id) & 1)) continue;
-        mres |= 1u << k;
-        if (id < 64) used |= 1ull << id;
+        if ((mres >> k) & 1) continue;
+        if (id < MFG_WAVE * NW && mask_get(used, id)) continue;
+        mres |= 1ull << k;
+        if (id < MFG_WAVE * NW) mask_set(used, id);
       }
     };
     // candidate cells first, lane-parallel (lane = door, then lane = agent); the ordered passes below
     // visit only cells with >= 2 colliders (usually none)
     const int nd = S->nd;
-    const int dcnt = nd ? door_cell_counts(e, e.scratch, true) : 0;  // whole wave: every lane adds its entities
-    const u64 dcand = ballot(e.lane < nd && dcnt >= 2);
-    const int myp = e.lane < A ? e.agpos()[e.lane] : -1;
+    int dcnt[NW];
+    if (nd) door_cell_counts<NW>(e, e.scratch, true, dcnt);  // whole wave: every lane adds its entities
+    u64 dcand[NW], acand[NW];
+    int myp[NW];
+#pragma unroll
+    for (int g = 0; g < NW; g++) {
+      dcand[g] = nd ? ballot(g * MFG_WAVE + e.lane < nd && dcnt[g] >= 2) : 0ull;
+      const int a = g * MFG_WAVE + e.lane;
+      myp[g] = a < A ? e.agpos()[a] : -1;
+    }
     // agents on non-door cells: the other agents on the same cell (readlane loop) + maintainers there
-    int na = 0;
-    for (int b = 0; b < A; b++) na += (rl(myp, b) == myp) ? 1 : 0;
     const int nkm = S->kmax ? e.H(H_N_MAINTS) : 0;
-    for (int k = 0; k < nkm; k++) { const int w = e.maints()[k]; na += (EW_POS(w) == myp && (w & EW_PRESENT)) ? 1 : 0; }
-    const u64 acand = ballot(e.lane < A && door_idx(e, myp < 0 ? 0 : myp) < 0 && na >= 2);
-    for (u64 dm = dcand; dm; dm &= dm - 1) {
-      const int d = ffs64(dm);
-      const int cell = S->door_cells[d];
-      hit = true;
-      if (present_closed_door(e, cell) && !((used >> d) & 1)) { o.door_coll |= 1ull << d; used |= 1ull << d; }
-      if (e.lane < A && e.agpos()[e.lane] == cell) agres = true;
-      maint_results(cell);
+#pragma unroll
+    for (int h = 0; h < NW; h++) {
+      int na = 0;
+#pragma unroll
+      for (int g = 0; g < NW; g++) {
+        const int ng = min(A - g * MFG_WAVE, MFG_WAVE);
+        for (int b = 0; b < ng; b++) na += (rl(myp[g], b) == myp[h]) ? 1 : 0;
+      }
+      for (int k = 0; k < nkm; k++) { const int w = e.maints()[k]; na += (EW_POS(w) == myp[h] && (w & EW_PRESENT)) ? 1 : 0; }
+      acand[h] = ballot(h * MFG_WAVE + e.lane < A && door_idx(e, myp[h] < 0 ? 0 : myp[h]) < 0 && na >= 2);
     }
-    for (u64 am = acand; am; am &= am - 1) {
-      const int a = ffs64(am);
-      const int cell = uni(e.agpos()[a]);
-      hit = true;
-      if (e.lane == a) agres = true;
-      maint_results(cell);
-    }
+#pragma unroll
+    for (int g = 0; g < NW; g++)
+      for (u64 dm = dcand[g]; dm; dm &= dm - 1) {
+        const int d = g * MFG_WAVE + ffs64(dm);
+        const int cell = S->door_cells[d];
+        hit = true;
+        if (present_closed_door(e, cell) && !mask_get(used, d)) { mask_set(o.door_coll, d); mask_set(used, d); }
+#pragma unroll
+        for (int h = 0; h < NW; h++)
+          if (h * MFG_WAVE + e.lane < A && myp[h] == cell) agres[h] = true;
+        maint_results(cell);
+      }
+#pragma unroll
+    for (int h = 0; h < NW; h++)
+      for (u64 am = acand[h]; am; am &= am - 1) {
+        const int l = ffs64(am);
+        const int cell = uni(e.agpos()[h * MFG_WAVE + l]);
+        hit = true;
+        if (e.lane == l) agres[h] = true;
+        maint_results(cell);
+      }
     for (int k = 0; k < nk; k++) {
       const int w = uni(e.maints()[k]);
       if (!(w & EW_PRESENT)) continue;
       const int cell = EW_POS(w);
-      if (door_idx(e, cell) >= 0 || colliders_at(e, cell) < 2) continue;
+      if (door_idx(e, cell) >= 0 || colliders_at<NW>(e, cell) < 2) continue;
       hit = true;
       maint_results(cell);
     }
-    if (agres) {
-      if (!(o.my_watch_ev & 1)) o.my_rew += ru.f[0];
-      o.my_watch_ev |= 1;
-    }
+#pragma unroll
+    for (int h = 0; h < NW; h++)
+      if (agres[h]) {
+        if (!(o.my_watch_ev[h] & 1)) o.my_rew[h] += ru.f[0];
+        o.my_watch_ev[h] |= 1;
+      }
     o.maint_coll |= mres;
     if (ru.i[0] && hit) o.done_mask |= (int)(1u << 31);  // curr_done -> on_check_done
   } else if (op == MFG_RULE_BATTERY_DECHARGE || op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:66-87
-    if (e.lane < S->A) {
-      const bool dis = e.bat()[e.lane] == 0.0;
-      int par = e.agpar()[e.lane];
-      if (dis) {
-        o.my_rew += ru.f[1];
-        o.my_watch_ev |= 2;
-        if (ru.i[0]) par |= 1 << ri;
+#pragma unroll
+    for (int h = 0; h < NW; h++) {
+      const int a = h * MFG_WAVE + e.lane;
+      if (a < S->A) {
+        const bool dis = e.bat()[a] == 0.0;
+        int par = e.agpar()[a];
+        if (dis) {
+          o.my_rew[h] += ru.f[1];
+          o.my_watch_ev[h] |= 2;
+          if (ru.i[0]) par |= 1 << ri;
+        }
+        if (par && !dis) par &= ~(1 << ri);
+        e.agpar()[a] = par;
       }
-      if (par && !dis) par &= ~(1 << ri);
-      e.agpar()[e.lane] = par;
     }
     wave_sync();
   }
 }
 
-__device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
+template <int NW>
+__device__ void rule_check_done(const Env& e, StepOut<NW>& o, int ri) {
   SpecP S = e.S;
   const CS mfg_rule& ru = S->s.rules[ri];
   const int op = ru.op;
@@ -1950,20 +1997,30 @@ __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
   } else if (op == MFG_RULE_WATCH_COLLISIONS) {
     if (ru.i[0] && (o.done_mask & (int)(1u << 31))) { o.done = 1; o.g_rew += ru.f[1]; }
   } else if (op == MFG_RULE_DONE_BATTERY) {  // batteries/rules.py:122-128
-    const bool dz = e.lane < S->A && e.bat()[e.lane] == 0.0;
-    const u64 m = ballot(dz);
-    const bool any = m != 0;
-    const bool all = popc(m) == S->A;
+    int nz = 0;
+#pragma unroll
+    for (int h = 0; h < NW; h++) {
+      const int a = h * MFG_WAVE + e.lane;
+      nz += popc(ballot(a < S->A && e.bat()[a < S->A ? a : 0] == 0.0));
+    }
+    const bool any = nz != 0;
+    const bool all = nz == S->A;
     if (ru.i[1] && (any || all)) { o.done = 1; o.done_mask |= 1 << ri; o.g_rew += ru.f[2]; }
   } else if (op == MFG_RULE_DONE_MAINT_COLLISION) {  // maintenance/rules.py:32-40
     const int nk = S->kmax ? e.H(H_N_MAINTS) : 0;
-    bool on = false;
-    if (e.lane < S->A) {
-      const int p = e.agpos()[e.lane];
-      for (int k = 0; k < nk; k++) on |= EW_POS(e.maints()[k]) == p;
+    bool any = false;
+#pragma unroll
+    for (int h = 0; h < NW; h++) {
+      const int a = h * MFG_WAVE + e.lane;
+      bool on = false;
+      if (a < S->A) {
+        const int p = e.agpos()[a];
+        for (int k = 0; k < nk; k++) on |= EW_POS(e.maints()[k]) == p;
+      }
+      if (on) { o.my_rew[h] += ru.f[0]; o.my_watch_ev[h] |= 4; }
+      any |= ballot(on) != 0;
     }
-    if (on) { o.my_rew += ru.f[0]; o.my_watch_ev |= 4; }
-    if (ballot(on)) { o.done = 1; o.done_mask |= 1 << ri; }
+    if (any) { o.done = 1; o.done_mask |= 1 << ri; }
   } else if (op == MFG_RULE_DONE_DIRT) {  // clean_up/rules.py:22-25
     if (e.H(H_N_DIRT) == 0 && e.H(H_STEP)) { o.done = 1; o.done_mask |= 1 << ri; o.g_rew += ru.f[0]; }
   } else if (op == MFG_RULE_DONE_DEST) {  // destinations/rules.py:73-92
@@ -1985,6 +2042,7 @@ __device__ void rule_check_done(const Env& e, StepOut& o, int ri) {
 // ------------------------------------------------------------------------------------------------
 // reset (factory.py:134-148; global_entities.py:196-203; rules.py:182-199; SpawnEntity rules)
 // ------------------------------------------------------------------------------------------------
+template <int NW>
 __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scratch) {
   SpecP S = e.S;
   const int A = S->A, W = S->s.W;
@@ -1992,10 +2050,14 @@ __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scra
   pay_debt(e);
   // OBSBuilder keeps the episode-1 agent / battery objects for its ray origins and bound layers
   if (e.H(H_OBS_INIT) && !e.H(H_FROZEN)) {
-    if (e.lane < A) {
-      e.forg()[e.lane] = e.agpos()[e.lane];
-      e.fgp()[e.lane] = e.agpos()[e.lane];
-      e.fbat()[e.lane] = e.bat()[e.lane];
+#pragma unroll
+    for (int h = 0; h < NW; h++) {
+      const int a = h * MFG_WAVE + e.lane;
+      if (a < A) {
+        e.forg()[a] = e.agpos()[a];
+        e.fgp()[a] = e.agpos()[a];
+        e.fbat()[a] = e.bat()[a];
+      }
     }
     e.setH(H_FROZEN, 1);
   }
@@ -2008,8 +2070,12 @@ __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scra
       e.mst(k)[MS_PATH_N] = 0; e.mst(k)[MS_PATH_HEAD] = 0; e.mst(k)[MS_NEXT_N] = 0; e.mst(k)[MS_LAST_SERVICED] = -1;
     }
   }
-  if (e.lane < S->nd) e.door()[e.lane] = DW_PRESENT | ((S->s.door_auto_close & 0xFF) << 8);  // closed
-  if (e.lane < A) { e.agpos()[e.lane] = -1; e.agpar()[e.lane] = 0; }
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int i = h * MFG_WAVE + e.lane;
+    if (i < S->nd) e.door()[i] = DW_PRESENT | ((S->s.door_auto_close & 0xFF) << 8);  // closed
+    if (i < A) { e.agpos()[i] = -1; e.agpar()[i] = 0; }
+  }
   wave_sync();
   // SpawnAgents: per agent empty_positions (floor shuffle + filter + shuffle of the list) then pop().
   // At this point the only occupants of floor-list cells (every non-wall cell, doors included) are the doors,
@@ -2017,7 +2083,7 @@ __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scra
   // iff it is no door and no earlier agent stands on it, so empty_positions has nf - nd - a cells and the pick
   // scan tests the door table and the earlier agents' cells (lane b holds agent b's cell) instead of every
   // entity group per cell.
-  int my_cell = -1;  // lane b < a: agent b's cell
+  int my_cell = -1;  // lane b < a: agent b's cell (agents 64.. are read from the record)
   for (int a = 0; a < A; a++) {
     floor_shuffle(e);
     const uint16_t* perm = e.perm();
@@ -2025,7 +2091,10 @@ __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scra
     const int m = nf - S->nd - a;
     auto empty_at = [&](int cell) {
       bool occ = S->door_of[cell] != 0xFF;
-      for (int b = 0; b < a; b++) occ |= rl(my_cell, b) == cell;
+      const int a0 = min(a, MFG_WAVE);
+      for (int b = 0; b < a0; b++) occ |= rl(my_cell, b) == cell;
+      if constexpr (NW > 1)
+        for (int b = MFG_WAVE; b < a; b++) occ |= e.agpos()[b] == cell;
       return !occ;
     };
     // the draws of shuffle(empty_positions) on the replay's branch-free chunked path; the first accepted draw
@@ -2071,7 +2140,9 @@ __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scra
     if (op == MFG_RULE_SPAWN_BATTERIES) {
       e.setH(H_BAT_BASE, e.H(H_CNT_BATTERY));
       e.setH(H_CNT_BATTERY, e.H(H_CNT_BATTERY) + A);
-      if (e.lane < A) e.bat()[e.lane] = S->s.battery_initial;
+#pragma unroll
+      for (int h = 0; h < NW; h++)
+        if (h * MFG_WAVE + e.lane < A) e.bat()[h * MFG_WAVE + e.lane] = S->s.battery_initial;
       wave_sync();
     } else if (op == MFG_RULE_SPAWN_PODS || op == MFG_RULE_SPAWN_DROPOFFS || op == MFG_RULE_SPAWN_ITEMS ||
                op == MFG_RULE_SPAWN_DESTS) {
@@ -2179,17 +2250,28 @@ __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scra
         wave_sync();
       }
       const int p = n ? uni(nb[n - 1]) : -1;
-      const u64 am = p >= 0 ? agents_at(e, p) : 0ull;
-      if (!am) { reset_crash = MFG_CRASH_RULE; break; }  // pop() on an empty list / assert isinstance(.., Agent)
       // get_first(by_pos(p)): the Agents group lists a cell's agents in arrival order
-      int arr = e.lane < A && ((am >> e.lane) & 1) ? e.agarr()[e.lane] : 0x7FFFFFFF;
+      int arr = 0x7FFFFFFF;
+#pragma unroll
+      for (int h = 0; h < NW; h++) {
+        const int b = h * MFG_WAVE + e.lane;
+        const bool on = p >= 0 && b < A && e.agpos()[b < A ? b : 0] == p;
+        arr = min(arr, on ? e.agarr()[b] : 0x7FFFFFFF);
+      }
       for (int o2 = 32; o2 > 0; o2 >>= 1) arr = min(arr, __shfl_xor(arr, o2));
-      const int a = ffs64(ballot(e.lane < A && ((am >> e.lane) & 1) && e.agarr()[e.lane < A ? e.lane : 0] == arr));
+      if (arr == 0x7FFFFFFF) { reset_crash = MFG_CRASH_RULE; break; }  // pop() on an empty list / assert isinstance
+      int a = -1;
+#pragma unroll
+      for (int h = NW - 1; h >= 0; h--) {
+        const int b = h * MFG_WAVE + e.lane;
+        const u64 am = ballot(b < A && e.agpos()[b < A ? b : 0] == p && e.agarr()[b < A ? b : 0] == arr);
+        if (am) a = h * MFG_WAVE + ffs64(am);
+      }
       // chosen_agent.move(free_pos) (entity.py:175-199): check_move_validity once (states.py:240-270, Q3)
-      const bool blocked = blocked_at(e, fp);
+      const bool blocked = blocked_at<NW>(e, fp);
       if (!blocked) floor_shuffle(e);
       const bool not_blocked = !blocked && S->level[fp] != 1;
-      const bool blocking_others = S->s.agent_blocking[a] && (colliders_at(e, fp) > 0 || blocked);
+      const bool blocking_others = S->s.agent_blocking[a] && (colliders_at<NW>(e, fp) > 0 || blocked);
       if (p != fp && not_blocked && !blocking_others) set_agent_pos(e, a, fp);
     }
   }
@@ -2262,9 +2344,9 @@ __device__ void build_cmap(const Env& e, int wv = 0, int nwv = 1) {
   for (int i = wv * MFG_WAVE + lane; i < n16; i += MFG_WAVE * nwv) ((uint4*)e.cmap)[i] = src[i];
   mw_sync<MW>();
   if (MW && wv) return;  // the dynamic entities: one wave (the others wait at the caller's barrier)
-  if (lane < S->nd) {
-    const int w = e.door()[lane];
-    if (w & DW_PRESENT) cmap_or<MM>(e, S->door_cells[lane], CM_DOOR | ((w & DW_OPEN) ? 0u : CM_DCLOSED));
+  for (int d = lane; d < S->nd; d += MFG_WAVE) {
+    const int w = e.door()[d];
+    if (w & DW_PRESENT) cmap_or<MM>(e, S->door_cells[d], CM_DOOR | ((w & DW_OPEN) ? 0u : CM_DCLOSED));
   }
   auto grp = [&](const int* tbl, int n, uint32_t bit, bool dest) {
     for (int i = lane; i < n; i += MFG_WAVE) {
@@ -2421,8 +2503,9 @@ template <bool LR>
 using obs_u32 = typename std::conditional<LR, uint32_t, lds_u32>::type;
 template <typename DP>
 struct SupT {  // per-agent suppression sets from the identifier dedupe
-  u64 items, pods, drops, dests, doors, machines, maints;
-  uint8_t* wsup;   // [dd] window cells whose wall is suppressed (walls outside the window are never placed)
+  u64 items, pods, drops, dests, machines, maints;
+  uint8_t* wsup;   // [dd] window cells whose wall or door is suppressed (both are static cells, one per cell; entities
+                   // outside the window are never placed)
   DP* dsup;        // dirt slots: bitmap [dirt_cap / 32] (LDS; HBM in the long-ray render)
   int wx0, wy0, oh, ow, W;  // window origin cell and shape
   __device__ __forceinline__ bool dirt_sup(int i) const {
@@ -2441,10 +2524,9 @@ __device__ __forceinline__ void sup_add(SupT<DP>& s, int code, int xy, int lane)
     case K_DIRT:
       if (lane == 0) s.dsup[slot >> 5] |= 1u << (slot & 31);
       break;
-    case K_DOOR: s.doors |= bit; break;
     case K_MACHINE: s.machines |= bit; break;
     case K_MAINT: s.maints |= bit; break;
-    default: {
+    default: {  // a wall (K_WALL) or a door (K_DOOR): xy is its cell
       const int px = (xy >> 16) - s.wx0, py = (xy & 0xFFFF) - s.wy0;
       if (px >= 0 && py >= 0 && px < s.oh && py < s.ow && lane == 0) s.wsup[px * s.ow + py] = 1;
       break;
@@ -2511,9 +2593,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   const PairList pairs{(lds_int*)e.scratch, (glb_int*)pair_glob, S->pairs_lds};
   int npairs = 0;
   if (!MW || wv == 0) {
-#ifndef MFG_ABLATE_OB_NODEDUP
     npairs = build_id_pairs<MM>(e, pairs);
-#endif
     for (int q = lane; q < npairs; q += MFG_WAVE) {  // cells -> packed (x << 16 | y), agent independent
       const int cA = pairs.get(q, 0), cB = pairs.get(q, 1);
       pairs.set(q, 0, ((cA / W) << 16) | (cA % W));
@@ -2538,12 +2618,15 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   // dirt suppression bitmap for groups wider than a wave: after the per-lane sink words of the ray walk
   tu32* dsup = (tu32*)((uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE);
   const int ndsup = S->dirt_cap >> 5;
-  // agents on each window cell: [dd][2] u32 (bit b = agent b), filled by a lane-per-agent scatter
+  // agents on each window cell: [dd][2] u32 (bit b = agent b), filled by a lane-per-agent scatter; specs with more
+  // than 64 agents (wide) have a second table for agents 64..127 right after it (amw2)
   tu32* amw = dsup + ndsup;
+  const bool wide = S->A > MFG_WAVE;
+  tu32* amw2 = amw + 2 * dd;
   // window dirt map (specs with dirt): per window cell 1 + the index of the last present, non-suppressed pile on
   // it, built per agent from the pile table (lane = pile), so the placement reads a cell's pile instead of
   // scanning every pile per 64-cell block (C5: up to 384 piles)
-  tu32* wdirt = amw + 2 * dd;
+  tu32* wdirt = amw + 2 * S->lane_passes * dd;
   // packed mode: queue of the agent row's nonzero entries awaiting the fused projection ([64] flat index, [64] value);
   // the weight rows of up to 4 entries are loaded together, so their L2 latencies overlap instead of chaining
   tu32* pq = wdirt + (DIRT ? dd : 0);
@@ -2559,7 +2642,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   tu32* ctag = pq + 2 * MFG_WAVE;
   constexpr bool has_dirt = DIRT;  // S->dirt_cap != 0 (a template parameter: the register budget of k_obs)
   const float invW = 1.0f / (float)W;
-  // lane-distributed copies of the small tables (uniform loops read them with v_readlane)
+  // lane-distributed copies of the small tables (uniform loops read them with v_readlane); agents 64.. of wide specs
+  // are read from the record image per agent
   const int agp = lane < A ? e.agpos()[lane] : -1;
   const int org_l = lane < A ? (frozen ? e.forg()[lane] : agp) : -1;
   const int nT = e.H(H_N_DIRT);
@@ -2578,7 +2662,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   int pf_ofl = -1;
   uint32_t pf_b = 0, pf_c = 0, pf_d = 0;
   auto rs_fetch = [&](int ag) {
-    pf_ofl = S->ray_static ? uni((int)S->cell_f[rl(orgx, ag) * W + rl(orgy, ag)]) : -1;
+    const int og = ag < MFG_WAVE ? rl(orgx, ag) * W + rl(orgy, ag) : uni(frozen ? e.forg()[ag] : e.agpos()[ag]);
+    pf_ofl = S->ray_static ? uni((int)S->cell_f[og]) : -1;
     if (pf_ofl >= 0) {
       const bool has = lane < S->nrays;
       const uint32_t* rs = S->ray_static + ((size_t)pf_ofl * S->nrays + (has ? lane : 0)) * 3;
@@ -2589,19 +2674,24 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   };
   if constexpr (PREFETCH_RS) rs_fetch(MW ? wv : 0);
   for (int a = MW ? wv : 0; a < A; a += MW ? nwv : 1) {
-    const int apos = rl(agp, a);
-    const int ax = rl(agx, a), ay = rl(agy, a);
-    const int ox = rl(orgx, a), oy = rl(orgy, a);
+    int apos, ax, ay, ox, oy;
+    if (a < MFG_WAVE) {
+      apos = rl(agp, a);
+      ax = rl(agx, a); ay = rl(agy, a);
+      ox = rl(orgx, a); oy = rl(orgy, a);
+    } else {  // agents 64..127 of a wide spec
+      apos = uni(e.agpos()[a]);
+      const int og = frozen ? uni(e.forg()[a]) : apos;
+      ax = apos / W; ay = apos - ax * W;
+      ox = og / W; oy = og - ox * W;
+    }
     const int wx0 = full ? 0 : ax - S->r, wy0 = full ? 0 : ay - S->r;
     // origin floor index (static table)
     const int ofl = PREFETCH_RS ? pf_ofl : (S->ray_static ? uni((int)S->cell_f[ox * W + oy]) : -1);
-#ifdef MFG_ABLATE_OB_NOINIT  // timing only: the per-agent tables are cleared for the first agent only
-    if (a == (MW ? wv : 0))
-#endif
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
-    for (int i = lane; i < 2 * dd; i += MFG_WAVE) amw[i] = 0u;
+    for (int i = lane; i < 2 * S->lane_passes * dd; i += MFG_WAVE) amw[i] = 0u;
     if (has_dirt)
       for (int i = lane; i < dd; i += MFG_WAVE) wdirt[i] = 0u;
     tbl_sync<LR>();
@@ -2610,11 +2700,13 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       if ((unsigned)wx < (unsigned)oh && (unsigned)wy < (unsigned)ow)
         atomicOr((uint32_t*)&amw[2 * (wx * ow + wy) + (lane >> 5)], 1u << (lane & 31));
     }
+    if (wide && lane + MFG_WAVE < A) {  // agents 64..127
+      const int p2 = e.agpos()[lane + MFG_WAVE];
+      const int wx = p2 / W - wx0, wy = p2 % W - wy0;
+      if ((unsigned)wx < (unsigned)oh && (unsigned)wy < (unsigned)ow)
+        atomicOr((uint32_t*)&amw2[2 * (wx * ow + wy) + (lane >> 5)], 1u << (lane & 31));
+    }
     // ---- ray walk (lane = ray, 64 rays per pass): blocking bits first, then the walk on bitmasks ----
-#ifdef MFG_ABLATE_OB_NORAY
-    for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0u;
-    if (0)
-#endif
     if constexpr (LR) {
       // long rays: each lane walks its ray in 32-point segments (points from the 16-bit table, dx | dy << 16),
       // carrying whether the walk has stopped and the previous point (the diagonal cut of a segment's first point);
@@ -2730,13 +2822,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     tbl_sync<LR>();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     SupT<tu32> sup;
-    sup.items = sup.pods = sup.drops = sup.dests = sup.doors = sup.machines = sup.maints = 0;
+    sup.items = sup.pods = sup.drops = sup.dests = sup.machines = sup.maints = 0;
     sup.wx0 = wx0; sup.wy0 = wy0; sup.oh = oh; sup.ow = ow; sup.W = W;
     sup.wsup = wsup;
     sup.dsup = dsup;
-#ifdef MFG_ABLATE_OB_NOPAIRTEST
-    if (0)
-#endif
     for (int q0 = 0; q0 < npairs; q0 += MFG_WAVE) {
       const int q = q0 + lane;
       // the first pass's pair cells stay in registers across agents (the usual single pass)
@@ -2829,9 +2918,6 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       }
     }
     // ---- placement (lane = window cell, 64 cells per pass): tag bits from the cell map ----
-#ifdef MFG_ABLATE_OB_NOPLACE
-    if (0)
-#endif
     for (int w0 = 0; w0 < dd; w0 += MFG_WAVE) {
       // dense (and FLAT): lanes past the window repeat the last window cell (its value, to its address), so the layer
       // stores need no exec mask; the per-layer packed placement keeps them out (its ballots count entries)
@@ -2852,13 +2938,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       const uint32_t m = v ? mraw : 0u;
       const bool wall_sup = wsup[inwin ? wi : 0] != 0;
       // bit t = tag t (< 16) has a (not suppressed) entity here: the cell-map bits are the tag bits
-      uint32_t tags = m & ((wall_sup ? 0u : CM_WALL) | CM_DOOR | CM_ITEM | CM_POD | CM_DROP | CM_DIRT | CM_DEST);
+      // (wall_sup: the cell's wall or door lost an identifier dedupe; a cell holds at most one of the two)
+      uint32_t tags = m & ((wall_sup ? 0u : CM_WALL | CM_DOOR) | CM_ITEM | CM_POD | CM_DROP | CM_DIRT | CM_DEST);
       if (MM) tags |= (m >> 1) & ((1u << MFG_TAG_MACHINES) | (1u << MFG_TAG_MAINTAINERS));
       // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
-#ifdef MFG_ABLATE_OB_NORESUP  // timing only: the identifier-dedupe suppressions are not applied to the placement
-      sup.doors = sup.items = sup.pods = sup.drops = sup.dests = sup.machines = sup.maints = 0;
-#endif
-      if (sup.doors && (m & CM_DOOR) && ((sup.doors >> door_idx(e, cell)) & 1)) tags &= ~(1u << MFG_TAG_DOORS);
       auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
         if (!sm) return;
         bool any = false;
@@ -2886,6 +2969,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
       // 0.4444 open, dirt = amount)
       auto tagv = [&](int tag) -> double {
+        if (tag >= MFG_TAG_AGENT0 + MFG_WAVE) {  // agents 64..127 (wide specs): the second mask table
+          const int b = tag - MFG_TAG_AGENT0 - MFG_WAVE;
+          return (v && ((amw2[2 * wic + (b >> 5)] >> (b & 31)) & 1u)) ? 1.0 : 0.0;
+        }
         if (tag >= MFG_TAG_AGENT0) return ((amask >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
         if (!((tags >> tag) & 1u)) return 0.0;
         if (tag == MFG_TAG_DOORS) return (m & CM_DCLOSED) ? 0.6666 : 0.4444;
@@ -2897,6 +2984,11 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         ctag[wi] = tags | ((m & CM_DCLOSED) ? CT_CLOSED : 0u);
         amw[2 * wi] = (uint32_t)amask;
         amw[2 * wi + 1] = (uint32_t)(amask >> 32);
+        if (wide) {
+          const uint32_t w0v = amw2[2 * wi], w1v = amw2[2 * wi + 1];
+          amw2[2 * wi] = v ? w0v : 0u;
+          amw2[2 * wi + 1] = v ? w1v : 0u;
+        }
         if (has_dirt) wdirt[wi] = v ? wdirt[wi] : 0u;
         continue;
       }
@@ -2905,7 +2997,13 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         const uint32_t tf = (uint32_t)rl((int)lr_tf, l);
         const uint32_t ut = tf & 0xFFFFu, fl = tf >> 16;
         const uint64_t ab = (uint64_t)(uint32_t)rl((int)lr_alo, l) | ((uint64_t)(uint32_t)rl((int)lr_ahi, l) << 32);
-        OT out = (OT)(popc(tags & ut) + popc(amask & ab));  // a small count: exact in OT
+        int cnt = popc(tags & ut) + popc(amask & ab);
+        if (wide) {  // agents 64..127: the layer's second agent word (uniform load) against the second mask table
+          const uint64_t ab2 = ((const MfgLayerRec CS*)S->lrec + (size_t)a * S->lmax + l)->agent_bits2;
+          const u64 am2 = v ? ((u64)amw2[2 * wic] | ((u64)amw2[2 * wic + 1] << 32)) : 0ull;
+          cnt += popc(am2 & ab2);
+        }
+        OT out = (OT)cnt;  // a small count: exact in OT
         if (fl) {
           double val = 0.0;
           if (fl & LR_DOOR) {
@@ -2955,9 +3053,6 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         // for these stores (1.00x with MFG_OBS_NT=0): the 49-lane layer rows are not 64-B aligned.
         // Packing rows into aligned 64-lane stores (ds_bpermute) cut that to 1.14x but cost 67 VGPRs
         // and k_obs 0.494 -> 0.543 ms, so it was dropped (k_obs).
-#if defined(MFG_ABLATE_OB_NOSTORE)  // timing only: the values are computed, (almost) never stored
-        if (inwin && out == (OT)-12345.0) *op = out;
-#else
 #ifndef MFG_OBS_PLAIN_PTS
 #define MFG_OBS_PLAIN_PTS 12
 #endif
@@ -2972,7 +3067,6 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         } else {
           if (inwin) __builtin_nontemporal_store(out, op);
         }
-#endif
       }
     }
     if constexpr (FLAT) {
@@ -2991,9 +3085,18 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         const uint32_t tf = bperm(l, lr_tf);
         const uint64_t ab = (uint64_t)bperm(l, lr_alo) | ((uint64_t)bperm(l, lr_ahi) << 32);
         const uint32_t ut = tf & 0xFFFFu, fl = tf >> 16;
-        OT out = (OT)(popc(ct & ut) + popc(am & ab));  // a small count: exact in OT
+        int cnt = popc(ct & ut) + popc(am & ab);
+        if (wide) {  // agents 64..127: layer l's second agent word (per-lane load) against the second mask table
+          const uint64_t ab2 = ((const MfgLayerRec*)S->lrec + (size_t)a * S->lmax + l)->agent_bits2;
+          cnt += popc(((u64)amw2[2 * c] | ((u64)amw2[2 * c + 1] << 32)) & ab2);
+        }
+        OT out = (OT)cnt;  // a small count: exact in OT
         if (fl) {
           auto tagv = [&](int tag) -> double {
+            if (tag >= MFG_TAG_AGENT0 + MFG_WAVE) {  // agents 64..127 (wide specs): the second mask table
+              const int b = tag - MFG_TAG_AGENT0 - MFG_WAVE;
+              return ((amw2[2 * c + (b >> 5)] >> (b & 31)) & 1u) ? 1.0 : 0.0;
+            }
             if (tag >= MFG_TAG_AGENT0) return ((am >> (tag - MFG_TAG_AGENT0)) & 1) ? 1.0 : 0.0;
             if (!((ct >> tag) & 1u)) return 0.0;
             if (tag == MFG_TAG_DOORS) return (ct & CT_CLOSED) ? 0.6666 : 0.4444;
@@ -3044,14 +3147,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
           }
           continue;
         }
-#if defined(MFG_ABLATE_OB_NOSTORE)
-        if (out == (OT)-12345.0) out_a[el] = out;
-#else
         // non-temporal for every render: the 64-value runs leave at most the two edge lines of a run partial, so
         // the L2 merge that made plain stores pay for the per-layer rows of the multi-wave render is not needed
         // (C4 isolated k_obs 1.54 -> 1.36 ms, C4 10.72M -> 11.16M env-steps/s, profiles/r05_c4_flat_nt_ab.json)
         __builtin_nontemporal_store(out, out_a + el);
-#endif
       }
     }
     if constexpr (PK) {
@@ -3082,31 +3181,35 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
 // ------------------------------------------------------------------------------------------------
 #define MFG_EV_MISC MFG_EV_MISC_N
 
-template <bool RNG, bool MAINT>
-__device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
+template <bool RNG, bool MAINT, int NW>
+__device__ void env_step(const Env& e, const int (&my_act)[NW], StepOut<NW>& o, int* scratch) {
   SpecP S = e.S;
   const int A = S->A;
-  o.my_rew = 0.0; o.g_rew = 0.0; o.my_act_ev = 0; o.my_watch_ev = 0; o.door_coll = 0; o.maint_coll = 0;
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    o.my_rew[h] = 0.0; o.my_act_ev[h] = 0; o.my_watch_ev[h] = 0; o.my_slot[h] = -1; o.door_coll[h] = 0;
+  }
+  o.g_rew = 0.0; o.maint_coll = 0;
   o.respawn_items_value = -1; o.dirt_spawn_value = -1; o.dirt_spawn_valid = 0; o.door_autoclose = 0;
-  o.done_mask = 0; o.dest_reached = 0; o.crashed = 0; o.done = 0; o.my_slot = -1;
+  o.done_mask = 0; o.dest_reached = 0; o.crashed = 0; o.done = 0;
   e.setH(H_STEP, e.H(H_STEP) + 1);
   e.setH(H_TOTAL_STEPS, e.H(H_TOTAL_STEPS) + 1);
   o.crashed = e.H(H_CRASHED);  // a crash the reset hit (or a crashed env stepped without a reset): done, no step
   wave_sync();
-  const int a0 = o.crashed ? A : act_parallel(e, my_act, o);
+  const int a0 = o.crashed ? A : act_parallel<NW>(e, my_act, o);
   for (int a = a0; a < A && !o.crashed; a++) {
     if (uni(e.agpar()[a])) continue;  // paralyzed agents skip their action
-    const int slot = rl(my_act, a);
+    const int slot = agent_get(my_act, a);
     if (slot < 0 || slot >= S->s.n_actions[a]) { o.crashed = MFG_CRASH_ACTION; break; }  // IndexError upstream
-    do_action(e, o, a, slot);
-    if (e.lane == a) o.my_slot = slot;
+    do_action<NW>(e, o, a, slot);
+    agent_set(o.my_slot, a, e.lane, slot);
   }
   if (!o.crashed)
-    for (int q = 0; q < S->n_ph[0] && !o.crashed; q++) rule_tick_step<RNG, MAINT>(e, o, S->ph_rule[0][q], scratch);
+    for (int q = 0; q < S->n_ph[0] && !o.crashed; q++) rule_tick_step<RNG, MAINT, NW>(e, o, S->ph_rule[0][q], scratch);
   if (!o.crashed)
-    for (int q = 0; q < S->n_ph[1] && !o.crashed; q++) rule_post_step(e, o, S->ph_rule[1][q]);
+    for (int q = 0; q < S->n_ph[1] && !o.crashed; q++) rule_post_step<NW>(e, o, S->ph_rule[1][q]);
   if (!o.crashed)
-    for (int q = 0; q < S->n_ph[2]; q++) rule_check_done(e, o, S->ph_rule[2][q]);
+    for (int q = 0; q < S->n_ph[2]; q++) rule_check_done<NW>(e, o, S->ph_rule[2][q]);
   // the step's membership-only shuffles stay as debt: paid by k_replay after the launch, or inline by
   // the next order-dependent consumer (spawn / reset)
   if (o.crashed || e.H(H_OVERFLOW)) {  // H_CRASHED keeps the reason (MFG_CRASH_*, include/mfg.h)
@@ -3117,20 +3220,25 @@ __device__ void env_step(const Env& e, int my_act, StepOut& o, int* scratch) {
   wave_sync();
 }
 
-__device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& o, size_t row, double* reward,
+template <int NW>
+__device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut<NW>& o, size_t row, double* reward,
                                                    uint8_t* done, uint8_t* ev_act, uint8_t* ev_watch,
                                                    int32_t* ev_misc) {
   const int A = e.S->A;
-  if (e.lane < A) {
-    if (reward) reward[row * A + e.lane] = o.my_rew + o.g_rew;
-    if (ev_act) ev_act[row * A + e.lane] = (uint8_t)o.my_act_ev;
-    if (ev_watch) ev_watch[row * A + e.lane] = (uint8_t)o.my_watch_ev;
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int a = h * MFG_WAVE + e.lane;
+    if (a < A) {
+      if (reward) reward[row * A + a] = o.my_rew[h] + o.g_rew;
+      if (ev_act) ev_act[row * A + a] = (uint8_t)o.my_act_ev[h];
+      if (ev_watch) ev_watch[row * A + a] = (uint8_t)o.my_watch_ev[h];
+    }
   }
   if (e.lane == 0 && done) done[row] = (uint8_t)o.done;
-  if (ev_misc) {  // one 12-lane store (lane k writes slot k) instead of 12 single-lane stores
+  if (ev_misc) {  // one 16-lane store (lane k writes slot k) instead of 16 single-lane stores
     const int l = e.lane;
-    int v = (int)(uint32_t)o.door_coll;
-    v = l == 1 ? (int)(uint32_t)(o.door_coll >> 32) : v;
+    int v = (int)(uint32_t)o.door_coll[0];
+    v = l == 1 ? (int)(uint32_t)(o.door_coll[0] >> 32) : v;
     v = l == 2 ? o.respawn_items_value : v;
     v = l == 3 ? o.dirt_spawn_value : v;
     v = l == 4 ? o.dirt_spawn_valid : v;
@@ -3139,9 +3247,13 @@ __device__ __forceinline__ void write_step_outputs(const Env& e, const StepOut& 
     v = l == 7 ? o.done_mask : v;
     v = l == 8 ? e.hdr()[H_STEP] : v;
     v = l == 9 ? e.hdr()[H_EPISODE] : v;
-    v = l == 10 ? (int32_t)o.maint_coll : v;
+    v = l == 10 ? (int32_t)(uint32_t)o.maint_coll : v;
     v = l == 11 ? (e.S->kmax ? e.hdr()[H_MAINT_BASE] : 0) : v;
-    static_assert(MFG_EV_MISC == 12, "ev_misc row width");
+    v = l == 12 ? (NW > 1 ? (int)(uint32_t)o.door_coll[NW - 1] : 0) : v;
+    v = l == 13 ? (NW > 1 ? (int)(uint32_t)(o.door_coll[NW - 1] >> 32) : 0) : v;
+    v = l == 14 ? (int32_t)(uint32_t)(o.maint_coll >> 32) : v;
+    v = l == 15 ? 0 : v;
+    static_assert(MFG_EV_MISC == 16, "ev_misc row width");
     if (e.lane < MFG_EV_MISC) ev_misc[row * MFG_EV_MISC + e.lane] = v;
   }
 }
@@ -3202,6 +3314,7 @@ __device__ __forceinline__ void prefix_copy(uint8_t* dst, const uint8_t* src, Sp
 // creation (init=1): random.seed(py_seed), Factory.__init__ (floor list, OBSBuilder shuffle); then reset.
 // The first observation is rendered by k_obs afterwards.
 #ifndef MFG_OBS_UNIT  // host-unit kernel (not compiled in the render units)
+template <int NW>
 static __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec* S_, uint8_t* state, long long B,
                                                         const uint8_t* mask, int init, unsigned long long seed_base) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -3236,7 +3349,9 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec*
       e.pcg()[0] = S->pcg_init_hi; e.pcg()[1] = S->pcg_init_lo;
       e.pcg()[2] = S->pcg_inc_hi;  e.pcg()[3] = S->pcg_inc_lo;
     }
-    if (e.lane < S->nd) e.door()[e.lane] = DW_PRESENT;
+#pragma unroll
+    for (int h = 0; h < NW; h++)
+      if (h * MFG_WAVE + e.lane < S->nd) e.door()[h * MFG_WAVE + e.lane] = DW_PRESENT;
     for (int r = 0; r < S->s.n_rules; r++) {
       const CS mfg_rule& ru = S->s.rules[r];
       if (e.lane == 0 && ru.op == MFG_RULE_RESPAWN_ITEMS) e.rctr()[r] = ru.i[1];
@@ -3250,7 +3365,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec*
     wave_sync();
   }
   if (!(init & MFG_INIT_NO_RESET)) {
-    env_reset(e, e.scratch);
+    env_reset<NW>(e, e.scratch);
     e.setH(H_OBS_INIT, 1);  // the reference renders right after every reset
   }
   e.setH(H_DONE, 0);
@@ -3262,7 +3377,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec*
 // One env-step of every env (no reset, no render). FULL: the spec consumes the floor order inside a
 // step (S->step_rng), so the whole record incl. MT/perm is staged; otherwise only the lean prefix.
 #ifndef MFG_OBS_UNIT  // host-unit kernel (not compiled in the render units)
-template <bool FULL, bool MAINT, int SEL = 0>
+template <bool FULL, bool MAINT, int SEL, int NW>
 static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAINT ? 1 : 8) k_logic(const MfgDevSpec* S_, uint8_t* state, long long B,
                                                         const int32_t* actions, unsigned philox_seed,
                                                         unsigned env_base, long long step, double* reward,
@@ -3304,7 +3419,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   // after it instead of at their record offset (mdelta), then the count scratch: no MT, permutation or BFS scratch
   constexpr bool lm = MAINT && SEL == 1;
   const int ms0 = S->L.o_mstate & ~15, mlen = lm ? ((S->L.o_grank + 15) & ~15) - ms0 : 0;
-  uint8_t* slice = smem + (size_t)wid * (lm ? S->L.o_logic + mlen + 4 * MFG_WAVE : S->lds_logic);
+  uint8_t* slice = smem + (size_t)wid * (lm ? S->L.o_logic + mlen + 4 * MFG_WAVE * NW : S->lds_logic);
   constexpr bool full = FULL && !lm;
   if (full) {
     env_full(S, slice, e, env);
@@ -3332,13 +3447,18 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   const int nd0 = trim ? min(uni(((const int*)(rec + S->L.o_hdr))[H_N_DIRT]), S->dirt_cap) : 0;
   // the actions (a buffer load or Philox) while the record load is in flight
   const int A = S->A;
-  int my_act = 0;
-  if (e.lane < A) {
-    if (actions) {
-      my_act = actions[(size_t)env * A + e.lane];
-    } else {
-      const uint32_t u = philox_u32(philox_seed, env_base + (uint32_t)env, (uint32_t)step, (uint32_t)e.lane);
-      my_act = (int)(((uint64_t)u * (uint64_t)S->s.n_actions[e.lane]) >> 32);
+  int my_act[NW];
+#pragma unroll
+  for (int h = 0; h < NW; h++) {
+    const int a = h * MFG_WAVE + e.lane;
+    my_act[h] = 0;
+    if (a < A) {
+      if (actions) {
+        my_act[h] = actions[(size_t)env * A + a];
+      } else {
+        const uint32_t u = philox_u32(philox_seed, env_base + (uint32_t)env, (uint32_t)step, (uint32_t)a);
+        my_act[h] = (int)(((uint64_t)u * (uint64_t)S->s.n_actions[a]) >> 32);
+      }
     }
   }
   if (one_pass) {
@@ -3363,8 +3483,8 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
       wave_sync();
     }
   }
-  StepOut o;
-  env_step<FULL, MAINT>(e, my_act, o, e.scratch);
+  StepOut<NW> o;
+  env_step<FULL, MAINT, NW>(e, my_act, o, e.scratch);
   write_step_outputs(e, o, (size_t)env, reward, done, ev_act, ev_watch, ev_misc);
   if (e.lane == 0) S->rd_flag[env] = (o.done && auto_reset) ? 1 : 0;
   if (o.done && auto_reset) {
@@ -3398,6 +3518,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
 // Factory.reset(). A fixed grid of waves strides over the list (count <= B, every wave exits), so a step
 // with few episode ends costs a few waves instead of one wave per env.
 #ifndef MFG_OBS_UNIT  // host-unit kernel (not compiled in the render units)
+template <int NW>
 static __global__ void __launch_bounds__(MFG_WPB * 64) __attribute__((amdgpu_waves_per_eu(4)))
 k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B, int rd_slot) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -3415,7 +3536,7 @@ k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B, int rd_slot) {
     env_full(S, smem + (size_t)wid * S->lds_full, e, env);
     rec_copy(e.lds, rec, S->L.size, e.lane);
     wave_sync();
-    env_reset(e, e.scratch);
+    env_reset<NW>(e, e.scratch);
     e.setH(H_DONE, 0);
     wave_sync();
     rec_copy(rec, e.lds, S->L.size, e.lane);
@@ -3505,6 +3626,8 @@ static __global__ void __launch_bounds__(8 * 64) k_obs_mw_list(const MfgDevSpec*
 // resident grid of single-wave workgroups strides over every env (skip: envs left to the list render) or over a done
 // list; workgroup g owns HBM pool slot g for its per-agent tables (build_obs, LR), its LDS slice holds the lean record,
 // the cell map and the identifier pairs.
+// The done-list render (list != null, the engine's second stream) and the render of the other envs (the caller's
+// stream) may run at the same time: the list render owns slots [obs_slots, 2 obs_slots), the other one [0, obs_slots).
 template <typename OT, bool MM, int PK, bool DIRT>
 static __global__ void __launch_bounds__(MFG_WAVE) k_obs_lr(const MfgDevSpec* S_, const uint8_t* state, long long B,
                                                             OT* obs, ObsPacked pk, const uint8_t* skip,
@@ -3512,10 +3635,11 @@ static __global__ void __launch_bounds__(MFG_WAVE) k_obs_lr(const MfgDevSpec* S_
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   SpecP S = (SpecP)S_;
   const long long n = list ? min((long long)uni(list[0]), B) : B;
+  const int slot = (int)blockIdx.x + (list ? S->obs_slots : 0);  // gridDim.x <= obs_slots (launch_obs_t)
   for (long long q = blockIdx.x; q < n; q += gridDim.x) {
     const long long env = list ? (long long)uni(list[2 + q]) : q;
     if (env < 0 || env >= B || (!list && skip && skip[env])) continue;
-    obs_env<0, OT, MM, PK, DIRT>(S, smem, state, env, obs, pk, 0, 1, (int)blockIdx.x);
+    obs_env<0, OT, MM, PK, DIRT>(S, smem, state, env, obs, pk, 0, 1, slot);
   }
 }
 // Render of the envs of a done list (rd_list row: [0] = count, [2..] = envs): a resident grid strides over it.
@@ -3558,10 +3682,8 @@ __device__ __forceinline__ void replay_env(SpecP S, uint8_t* slice, uint8_t* rec
   for (int i = e.lane; i < S->replay_stab_n; i += MFG_WAVE) e.stab[i] = 0u;
   wave_sync();
   if (S->xchg_ordered) {
-#ifndef MFG_ABLATE_NODEBT
     const int d = e.H(H_DEBT);
     for (int k = 0; k < d; k++) replay_shuffle(e, e.perm());
-#endif
     e.setH(H_DEBT, 0);
     wave_sync();
   } else {

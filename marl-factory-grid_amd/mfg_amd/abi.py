@@ -2,12 +2,12 @@
 tests/test_abi.py checks sizeof() against the compiled libraries."""
 import ctypes as C
 
-MAX_AGENTS = 64
+MAX_AGENTS = 128
 MAX_ACTIONS = 32
 MAX_LAYERS = 64
-MAX_COMBINED = 72
+MAX_COMBINED = 144
 MAX_RULES = 32
-MAX_DOORS = 64
+MAX_DOORS = 128
 MAX_POSITIONS = 64
 
 # action opcodes
@@ -33,11 +33,15 @@ LAYER_ZERO, LAYER_TAG, LAYER_COMBINED, LAYER_BATTERY, LAYER_GLOBALPOS = range(5)
 
 DEST_ANY, DEST_ALL, DEST_SIMULTANEOUS = range(3)
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 # ev_misc row (include/mfg.h MFG_EVM_*)
-EV_MISC_N = 12
+EV_MISC_N = 16
 (EVM_DOOR_COLL_LO, EVM_DOOR_COLL_HI, EVM_RESPAWN_ITEMS, EVM_DIRT_SPAWN, EVM_DIRT_VALID, EVM_DEST_REACHED, EVM_FLAGS,
- EVM_DONE_MASK, EVM_STEP, EVM_EPISODE, EVM_MAINT_COLL, EVM_MAINT_BASE) = range(EV_MISC_N)
+ EVM_DONE_MASK, EVM_STEP, EVM_EPISODE, EVM_MAINT_COLL, EVM_MAINT_BASE, EVM_DOOR_COLL_2, EVM_DOOR_COLL_3,
+ EVM_MAINT_COLL_HI, EVM_RESERVED) = range(EV_MISC_N)
+# the ev_misc column and bit of door d's / maintainer slot k's WatchCollisions result
+EVM_DOOR_COLS = (EVM_DOOR_COLL_LO, EVM_DOOR_COLL_HI, EVM_DOOR_COLL_2, EVM_DOOR_COLL_3)
+EVM_MAINT_COLS = (EVM_MAINT_COLL, EVM_MAINT_COLL_HI)
 # crash reasons (MFG_CRASH_*)
 CRASH_NAMES = {0: 'none', 1: 'reference crash path (DestAction on a destination Q17 / RespawnItems Q9)',
                2: 'maintainer route: no path', 3: 'maintainer: no free cell', 4: 'maintainer: empty target list',
@@ -111,6 +115,7 @@ class MfgEvents(C.Structure):
         ('act', C.c_uint8 * MAX_AGENTS),
         ('watch', C.c_uint8 * MAX_AGENTS),
         ('door_coll', C.c_uint64),
+        ('door_coll_hi', C.c_uint64),
         ('maint_coll', C.c_uint64),
         ('respawn_items_value', C.c_int32),
         ('dirt_spawn_value', C.c_int32),

@@ -87,7 +87,7 @@ def step_results(spec, actions, ev):
             for a, n in enumerate(names):
                 if watch[a] & 1:
                     out.append(Res(n, a, 'Collisions', reward=rf[0], valid=False, phase=POST, slot=ri))
-            dc, d = int(g('door_coll')), 0
+            dc, d = int(g('door_coll')) | (int(g('door_coll_hi')) << 64), 0  # doors 0..127
             while dc:
                 if dc & 1:
                     out.append(Res(f'Door[{d}]', -1, 'Collisions', reward=rf[0], valid=False, phase=POST, slot=ri))

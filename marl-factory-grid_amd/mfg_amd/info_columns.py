@@ -121,7 +121,6 @@ class InfoColumns:
         acted = (act & 0x80) != 0
         flags = misc[:, abi.EVM_FLAGS]
         dmask = misc[:, abi.EVM_DONE_MASK] & 0xFFFFFFFF
-        door_coll = (misc[:, abi.EVM_DOOR_COLL_LO] & 0xFFFFFFFF) | ((misc[:, abi.EVM_DOOR_COLL_HI] & 0xFFFFFFFF) << 32)
         # per-agent reward tables of the action results: value by slot (drop-off branch: aux0 / aux1)
         tabs = {}
 
@@ -175,12 +174,12 @@ class InfoColumns:
             elif kind == 'watch_bit':
                 a, bit, r = p
                 add(k, (watch[:, a] & bit) != 0, r)
-            elif kind == 'door_coll':
+            elif kind == 'door_coll':  # door d: bit d & 31 of the d >> 5-th door column
                 d, r = p
-                add(k, ((door_coll >> d) & 1) != 0, r)
+                add(k, ((misc[:, abi.EVM_DOOR_COLS[d >> 5]] >> (d & 31)) & 1) != 0, r)
             elif kind == 'maint_coll':
                 kk, r = p
-                add(k, ((misc[:, abi.EVM_MAINT_COLL] >> kk) & 1) != 0, r)
+                add(k, ((misc[:, abi.EVM_MAINT_COLS[kk >> 5]] >> (kk & 31)) & 1) != 0, r)
             elif kind == 'done_bit':
                 bit, r = p
                 add(k, ((dmask >> bit) & 1) != 0, r)

@@ -514,7 +514,13 @@ class BatchedA2C:
 
     ``graph=True``: the update (loss, backward, gradient clipping, RMSprop step and the window slide, ~1,300 launches)
     is captured once as a HIP graph after two eager warm-up updates on a side stream and replayed from then on (one
-    launch per update); the optimizer then keeps its step counters on the device (``capturable``)."""
+    launch per update); the optimizer then keeps its step counters on the device (``capturable``).
+
+    Read at window boundaries: ``episodes`` and ``reward_sum`` fold in a window's done flags and rewards in ``learn``
+    (once per window), so a monitor that reads them between two ``learn`` calls sees the previous window's totals.
+    The engine's floor-shuffle replay is deferred to the window's last step (``MFG_STEP_DEFER_REPLAY``): a state
+    snapshot (``export_state``) taken mid-window holds a non-reference MT state and floor order until that replay
+    (the step results are identical either way)."""
 
     def __init__(self, factory, net=None, n_steps=5, gamma=0.99, entropy_coef=0.01, vf_coef=0.5, gae_coef=0.0,
                  lr=3e-4, cap=32, obs_emb_size=96, action_emb_size=16, hidden_size=64, use_agent_embedding=False,

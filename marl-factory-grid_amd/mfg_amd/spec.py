@@ -2,7 +2,7 @@
 
 Mirrors the reference's config surface (same YAML schema, defaults and quirks):
   FactoryConfigParser       marl_factory_grid/utils/config_parser.py:16-274
-  LevelParser.do_init       marl_factory_grid/utils/level_parser.py:458-498
+  LevelParser.do_init       marl_factory_grid/utils/level_parser.py:62-102
   OBSBuilder layer naming   marl_factory_grid/utils/observation_builder.py:237-277
   RayCaster ray table       marl_factory_grid/utils/ray_caster.py:34-49,141-199
 Classes are resolved by their reference name to an engine opcode; a class the engine does not implement
@@ -184,7 +184,7 @@ class EnvSpec:
 
 
 def _parse_level(path: Path):
-    """helpers.py:168-183 parse_level + level_parser.py:442-456 argwhere order."""
+    """helpers.py:168-183 parse_level + level_parser.py:46-60 argwhere order."""
     with open(path) as f:
         rows = [list(line.strip()) for line in f.readlines()]
     if len(set(len(r) for r in rows)) > 1:
@@ -291,7 +291,7 @@ def compile_spec(config_path, custom_level_path: Optional[str] = None, custom_mo
         group_names.append(name)
     ekw = {k: (v or {}) for k, v in ents.items() if k != 'Defaults'}
     if 'Doors' in ekw and not len(doors):
-        raise UnsupportedSpec('Doors requires a D in the level (level_parser.py:492-494)')
+        raise UnsupportedSpec('Doors requires a D in the level (level_parser.py:96-98)')
 
     # ---- agents (config_parser.py:128-199) ----
     agents_conf = cfg['Agents']
@@ -594,6 +594,8 @@ def _to_c(es: EnvSpec) -> abi.MfgSpec:
         for j, (kind, tag) in enumerate(es.layer_prog[a]):
             s.layers[a][j].kind = kind
             s.layers[a][j].tag = tag
+        if len(es.combined[a]) > abi.MAX_COMBINED:
+            raise UnsupportedSpec(f'a Combined layer with more than {abi.MAX_COMBINED} members')
         s.combined_n[a] = len(es.combined[a])
         for j, t in enumerate(es.combined[a]):
             s.combined_tags[a][j] = t

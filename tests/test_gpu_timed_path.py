@@ -93,7 +93,8 @@ def _timed_path(odt):
                 assert bool(dn[k, j]) == d_ref, f'{tag} done'
                 ev = events_from_rows(ea[k, j], ew[k, j], em[k, j])
                 assert ev['act'] == list(ev_ref.act[:A]) and ev['watch'] == list(ev_ref.watch[:A]), f'{tag} events'
-                assert ev['door_coll'] == ev_ref.door_coll and ev['done_mask'] == ev_ref.done_mask, f'{tag} events'
+                assert ev['door_coll'] == ev_ref.door_coll and ev['door_coll_hi'] == ev_ref.door_coll_hi, f'{tag} events'
+                assert ev['done_mask'] == ev_ref.done_mask, f'{tag} events'
                 assert ev['step'] == ev_ref.step, f'{tag} step'
                 if d_ref:
                     ndone += 1

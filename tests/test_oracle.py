@@ -17,7 +17,8 @@ FIXTURES = [('large8', 'large8.yaml'), ('rooms4', 'rooms4.yaml'), ('simple1', 's
             ('corridor_quantity', 'corridor_quantity.yaml'), ('logic_stress', 'logic_stress.yaml'),
             ('clean_and_bring', 'clean_and_bring.yaml'), ('large_full', 'large_full.yaml'),
             ('grid128_r10', 'grid128_r10.yaml'), ('qquad_full', 'qquad_full.yaml'), ('grid128_r20', 'grid128_r20.yaml'),
-            ('grid128_full', 'grid128_full.yaml'), ('wide40', 'wide40.yaml')]
+            ('grid128_full', 'grid128_full.yaml'), ('wide40', 'wide40.yaml'),
+            ('qquad_doors', 'qquad_doors.yaml'), ('agents81', 'agents81.yaml')]
 
 
 def test_mt19937_matches_cpython():

@@ -72,7 +72,7 @@ def test_hip_library_exports_every_declared_symbol():
     for f in funcs:
         assert hasattr(lib, f), f'{f} declared in include/*.h but not exported'
     lib.mfg_abi_version.restype = C.c_int
-    assert lib.mfg_abi_version() == 4
+    assert lib.mfg_abi_version() == 5
 
 
 def _hip_lib():
@@ -98,7 +98,7 @@ def test_event_row_contract_matches_header():
     from mfg_amd import abi
     from mfg_amd.engine import EV_MISC
     h = _header_enum('MFG_EV')
-    assert h['MFG_EV_MISC_N'] == abi.EV_MISC_N == EV_MISC == 12
+    assert h['MFG_EV_MISC_N'] == abi.EV_MISC_N == EV_MISC == 16
     for k, v in h.items():
         if k.startswith('MFG_EVM_'):
             assert getattr(abi, k[4:]) == v, k
@@ -126,13 +126,17 @@ def test_decode_events_through_the_abi():
     misc[abi.EVM_EPISODE] = 2
     misc[abi.EVM_MAINT_COLL] = 6
     misc[abi.EVM_MAINT_BASE] = 40
+    misc[abi.EVM_DOOR_COLL_2] = 1 << 3  # door 67
+    misc[abi.EVM_DOOR_COLL_3] = -2147483648  # door 127
+    misc[abi.EVM_MAINT_COLL_HI] = 1  # maintainer slot 32
     ev = events_from_rows(act, watch, misc)
     assert ev['act'] == list(act) and ev['watch'] == list(watch)
     assert ev['door_coll'] == (1 | (1 << 31) | (5 << 32))
     assert ev['respawn_items_value'] == -1 and ev['dirt_spawn_value'] == 3 and ev['dirt_spawn_valid'] == 1
     assert ev['dest_reached'] == 3 and ev['door_autoclose'] == 1 and ev['crashed'] == 1
     assert ev['crash_reason'] == 8 and ev['done_mask'] == (-2147483648 | 4)
-    assert ev['step'] == 17 and ev['episode'] == 2 and ev['maint_coll'] == 6 and ev['maint_base'] == 40
+    assert ev['step'] == 17 and ev['episode'] == 2 and ev['maint_coll'] == (6 | (1 << 32)) and ev['maint_base'] == 40
+    assert ev['door_coll_hi'] == (1 << 3) | (1 << 63)
 
 
 def test_create_validates_spec_without_touching_the_gpu():
@@ -143,7 +147,7 @@ def test_create_validates_spec_without_touching_the_gpu():
     lib.mfg_create.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_void_p)]
     cases = [('n_actions', lambda c: c.n_actions.__setitem__(0, 33), 'n_actions'),
              ('n_layers', lambda c: c.n_layers.__setitem__(1, 65), 'n_layers'),
-             ('combined_n', lambda c: c.combined_n.__setitem__(0, 100), 'combined_n'),
+             ('combined_n', lambda c: c.combined_n.__setitem__(0, 145), 'combined_n'),
              ('n_rules', lambda c: setattr(c, 'n_rules', 33), 'n_rules'),
              ('move arg', lambda c: setattr(c.actions[0][4], 'arg', 9), 'direction'),
              ('layer tag', lambda c: setattr(c.layers[0][2], 'tag', 99), 'tag'),
@@ -220,3 +224,28 @@ def test_capacity_limits(tmp_path, n_agents, extra_layers, n_noop, n_pos, error)
     else:
         with pytest.raises(UnsupportedSpec, match=error):
             compile_spec(cfg)
+
+
+@pytest.mark.parametrize('n_agents,error', [(81, None), (128, None), (129, 'agents > 128')])
+def test_agent_capacity(tmp_path, n_agents, error):
+    """Round 6: up to 128 agents (two 64-lane passes in the agent-parallel kernels; a Combined layer holds every
+    other agent), past that a clean refusal. The reference's Agents collection is positional and uncapped."""
+    from mfg_amd.spec import compile_spec, UnsupportedSpec
+    cfg = tmp_path / 'c.yaml'
+    cfg.write_text("General: {env_seed: 7, individual_rewards: true, level_name: large_qquad, pomdp_r: 2}\n"
+                   "Agents: {A: {Actions: [Noop, Move8, DoorUse], Observations: [{Combined: [Other, Walls]}, Doors], "
+                   f"Clones: {n_agents - 1}}}}}\nEntities: {{Doors: }}\nRules: {{}}\n")
+    if error is None:
+        s = compile_spec(cfg)
+        assert s.n_agents == n_agents and s.c.n_doors == 65 and max(s.n_layers) == 2
+        assert s.c.combined_n[n_agents - 1] == n_agents  # the other agents + Walls
+    else:
+        with pytest.raises(UnsupportedSpec, match=error):
+            compile_spec(cfg)
+
+
+def test_large_qquad_with_its_doors_compiles():
+    """VERDICT r5 missing 1: the reference's own large_qquad level keeps its 65 Doors (indices 0..64)."""
+    from mfg_amd.spec import compile_spec
+    s = compile_spec('qquad_doors.yaml')
+    assert s.c.n_doors == 65 and s.c.has_doors
