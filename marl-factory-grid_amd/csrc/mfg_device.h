@@ -83,8 +83,7 @@ struct MfgLayerRec {
   uint32_t unit_tags;  // entity tags (< 16) counted as 1.0
   uint32_t flags;      // LR_*: door / dirt / machine value of a single-tag layer, regex-bound layers, or a
                        // Combined layer that needs its ordered left-to-right f64 sum (non-unit members)
-  uint64_t agent_bits; // agents 0..63 counted as 1.0
-  uint64_t agent_bits2;// agents 64..127 (specs with more than 64 agents)
+  uint64_t agent_bits; // agents 0..63 counted as 1.0 (agents 64..127: MfgDevSpec::lrec_ab2)
 };
 
 struct MfgDevSpec {
@@ -152,6 +151,7 @@ struct MfgDevSpec {
   // NW template parameter of k_logic / k_reset / k_resetdone; the render branches on the agent count at run time)
   int32_t lane_passes;
   const MfgLayerRec* lrec;   // [A][lmax] layer records
+  const uint64_t* lrec_ab2;  // [A][lmax] the layer records' agents 64..127 counted as 1.0 (long-ray render only)
   // long-ray render (maxpts == 0: rays of 65..255 points, k_obs_lr): the ray table with 16-bit offsets, and the
   // per-agent tables (first-visit table, wall suppression, sinks, dirt bitmap, agent masks, dirt map, packed queue:
   // the same layout as the LDS render's per-wave part) of each resident render wave in HBM instead of LDS

@@ -384,7 +384,10 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     if (mp > 255) { delete e; return fail("rays longer than 255 points"); }
     static const int SIZES[] = {4, 6, 8, 10, 12, 14, 16, 18, 24, 32, 48, 64};
     h.maxpts = 0;  // 0: the long-ray render (k_obs_lr, 32-point segments of a 16-bit ray table)
-    for (int k : SIZES) if (k >= mp) { h.maxpts = k; break; }
+    // more than 64 agents: always the long-ray render, the one render compiled with the second agent word (its
+    // per-agent tables live in HBM pool slots, so they do not cost the other renders' occupancy)
+    if (s->n_agents <= MFG_WAVE)
+      for (int k : SIZES) if (k >= mp) { h.maxpts = k; break; }
     h.lrpts = h.maxpts ? 0 : align_up(mp, 32);
   }
   int lmax = 1;
@@ -475,7 +478,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   h.fv_words = align_up((2 * h.fr + 1) * (2 * h.fr + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
-              8 * h.lane_passes * h.dd +  // + per-window-cell agent masks (u64 per 64 agents)
+              8 * (s->n_agents > MFG_WAVE ? 2 : 1) * h.dd +  // + per-window-cell agent masks (u64 per 64 agents)
               (h.dirt_cap ? 4 * h.dd : 0) +  // + window dirt map
               8 * MFG_WAVE +  // + packed-mode projection queue
               (h.maxpts == 0 || h.maxpts <= MFG_OBS_FLAT_MAXPTS ? 4 * h.dd : 0);  // + stashed tag words (FLAT)
@@ -605,13 +608,14 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   rc |= upload(e, cell_f.data(), cell_f.size(), &h.cell_f);
   {  // layer records (MfgLayerRec)
     std::vector<MfgLayerRec> lrec((size_t)h.A * h.lmax);
+    std::vector<uint64_t> ab2((size_t)h.A * h.lmax, 0ull);
     for (int a = 0; a < h.A; a++)
       for (int l = 0; l < s->n_layers[a]; l++) {
         MfgLayerRec& R = lrec[(size_t)a * h.lmax + l];
-        R = MfgLayerRec{0u, 0u, 0ull, 0ull};
+        R = MfgLayerRec{0u, 0u, 0ull};
         const int kind = s->layers[a][l].kind, tag = s->layers[a][l].tag;
         if (kind == MFG_LAYER_TAG) {
-          if (tag >= MFG_TAG_AGENT0 + MFG_WAVE) R.agent_bits2 = 1ull << (tag - MFG_TAG_AGENT0 - MFG_WAVE);
+          if (tag >= MFG_TAG_AGENT0 + MFG_WAVE) ab2[(size_t)a * h.lmax + l] = 1ull << (tag - MFG_TAG_AGENT0 - MFG_WAVE);
           else if (tag >= MFG_TAG_AGENT0) R.agent_bits = 1ull << (tag - MFG_TAG_AGENT0);
           else if (tag == MFG_TAG_DOORS) R.flags = LR_DOOR;
           else if (tag == MFG_TAG_DIRT) R.flags = LR_DIRT;
@@ -621,7 +625,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
           if (h.comb_fast[a]) {
             R.unit_tags = h.comb_unit_tags[a];
             R.agent_bits = h.comb_agents[a];
-            R.agent_bits2 = h.comb_agents2[a];
+            ab2[(size_t)a * h.lmax + l] = h.comb_agents2[a];
           }
           else R.flags = LR_ORDERED;
         } else if (kind == MFG_LAYER_BATTERY) {
@@ -631,6 +635,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
         }
       }
     rc |= upload(e, lrec.data(), lrec.size(), &h.lrec);
+    rc |= upload(e, ab2.data(), ab2.size(), &h.lrec_ab2);
   }
   rc |= upload(e, node_ok.data(), node_ok.size(), &h.node_ok);
   rc |= upload(e, wd.data(), wd.size(), &h.wd_pairs);
@@ -1033,7 +1038,7 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
       // prefix + maintainer state/paths staged (no MT, permutation or BFS scratch: several times the occupancy), the
       // rest with the full record
       const int ms0 = e->h.L.o_mstate & ~15;
-      const int lm_lds = e->h.L.o_logic + (((e->h.L.o_grank + 15) & ~15) - ms0) + cnt_lds;
+      const int lm_lds = e->h.L.o_logic + (((e->h.L.o_mpath + 15) & ~15) - ms0) + cnt_lds;
       LAUNCH_LOGIC(true, true, 1, lm_lds);
       LAUNCH_LOGIC(true, true, 2, e->h.lds_logic);
     } else if (e->h.step_rng) {

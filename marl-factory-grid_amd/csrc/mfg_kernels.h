@@ -86,7 +86,8 @@ struct Env {
   uint8_t* bfs;     // maintainer BFS scratch (full-record kernels of specs with MoveMaintainers)
   int* hdrp;        // header slots (inside the record image, or a separate slice in k_replay)
   int lane;
-  int mdelta = 0;   // where the maintainer state/paths sit relative to their record offset (k_logic<.., SEL 1>)
+  int mdelta = 0;   // where the maintainer states sit relative to their record offset (k_logic<.., SEL 1>)
+  const uint16_t* gpath = nullptr;  // k_logic<.., SEL 1>: the maintainer paths read in place in the HBM record
   __device__ int* hdr() const { return hdrp; }
   __device__ int* rctr() const { return (int*)(lds + S->L.o_rule_ctr); }
   __device__ int* agpos() const { return (int*)(lds + S->L.o_agent_pos); }
@@ -110,7 +111,11 @@ struct Env {
   __device__ int* machines() const { return (int*)(lds + S->L.o_machines); }
   __device__ int* maints() const { return (int*)(lds + S->L.o_maints); }
   __device__ int* mst(int k) const { return (int*)(lds + S->L.o_mstate + mdelta) + k * S->mstate_ints; }
-  __device__ uint16_t* mpath(int k) const { return (uint16_t*)(lds + S->L.o_mpath + mdelta) + k * S->path_cap; }
+  __device__ uint16_t* mpath(int k) const { return (uint16_t*)(lds + S->L.o_mpath) + k * S->path_cap; }
+  // a maintainer's path cell for reading (in place in HBM in k_logic<.., SEL 1>, else the record image)
+  __device__ int mpath_at(int k, int i) const {
+    return gpath ? (int)gpath[(size_t)k * S->path_cap + i] : (int)mpath(k)[i];
+  }
   __device__ uint16_t* grank() const { return (uint16_t*)(lds + S->L.o_grank); }
   // uniform header access
   __device__ int H(int k) const { return uni(hdr()[k]); }
@@ -1719,7 +1724,7 @@ __device__ void maint_tick(const Env& e, int k, int* crashed) {
   }
   const int head = uni(st[MS_PATH_HEAD]);
   if (head >= uni(st[MS_PATH_N])) { *crashed = 5; return; }  // self._path[0] on an empty path
-  const int nxt = uni((int)e.mpath(k)[head]);
+  const int nxt = uni(e.mpath_at(k, head));
   const int d = door_idx(e, nxt);
   if (d >= 0 && !(e.door()[d] & DW_OPEN)) {  // _closed_door_in_path -> DoorUse
     door_use_at<NW>(e, pos / W, pos % W);
@@ -2528,7 +2533,7 @@ __device__ __forceinline__ void sup_add(SupT<DP>& s, int code, int xy, int lane)
     case K_MAINT: s.maints |= bit; break;
     default: {  // a wall (K_WALL) or a door (K_DOOR): xy is its cell
       const int px = (xy >> 16) - s.wx0, py = (xy & 0xFFFF) - s.wy0;
-      if (px >= 0 && py >= 0 && px < s.oh && py < s.ow && lane == 0) s.wsup[px * s.ow + py] = 1;
+      if (px >= 0 && py >= 0 && px < s.oh && py < s.ow && lane == 0) s.wsup[px * s.ow + py] = CM_WALL | CM_DOOR;
       break;
     }
   }
@@ -2613,20 +2618,21 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   uint32_t* fv = LR ? (uint32_t*)(S->obs_pool + (size_t)slot * (size_t)S->obs_slot_bytes)
                     : (uint32_t*)(e.scratch + 3 * S->pairs_lds + (MW ? wv * (S->lds_obs_wave >> 2) : 0));
   const int fw = 2 * fr + 1;
-  uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall the dedupe suppressed
+  uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall or door the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
   // dirt suppression bitmap for groups wider than a wave: after the per-lane sink words of the ray walk
   tu32* dsup = (tu32*)((uint32_t*)(wsup + ((dd + 15) & ~15)) + MFG_WAVE);
   const int ndsup = S->dirt_cap >> 5;
-  // agents on each window cell: [dd][2] u32 (bit b = agent b), filled by a lane-per-agent scatter; specs with more
-  // than 64 agents (wide) have a second table for agents 64..127 right after it (amw2)
+  // agents on each window cell: [dd][2] u32 (bit b = agent b), filled by a lane-per-agent scatter. Specs with more
+  // than 64 agents (wide) always take the long-ray render (mfg_create), whose tables have a second [dd][2] table for
+  // agents 64..127 (amw2); the other renders compile no wide code (their register budget is the C2-C5 one).
   tu32* amw = dsup + ndsup;
-  const bool wide = S->A > MFG_WAVE;
+  const bool wide = LR && S->A > MFG_WAVE;
   tu32* amw2 = amw + 2 * dd;
   // window dirt map (specs with dirt): per window cell 1 + the index of the last present, non-suppressed pile on
   // it, built per agent from the pile table (lane = pile), so the placement reads a cell's pile instead of
   // scanning every pile per 64-cell block (C5: up to 384 piles)
-  tu32* wdirt = amw + 2 * S->lane_passes * dd;
+  tu32* wdirt = amw + (wide ? 4 : 2) * dd;
   // packed mode: queue of the agent row's nonzero entries awaiting the fused projection ([64] flat index, [64] value);
   // the weight rows of up to 4 entries are loaded together, so their L2 latencies overlap instead of chaining
   tu32* pq = wdirt + (DIRT ? dd : 0);
@@ -2662,7 +2668,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   int pf_ofl = -1;
   uint32_t pf_b = 0, pf_c = 0, pf_d = 0;
   auto rs_fetch = [&](int ag) {
-    const int og = ag < MFG_WAVE ? rl(orgx, ag) * W + rl(orgy, ag) : uni(frozen ? e.forg()[ag] : e.agpos()[ag]);
+    const int og = (!LR || ag < MFG_WAVE) ? rl(orgx, ag) * W + rl(orgy, ag) : uni(frozen ? e.forg()[ag] : e.agpos()[ag]);
     pf_ofl = S->ray_static ? uni((int)S->cell_f[og]) : -1;
     if (pf_ofl >= 0) {
       const bool has = lane < S->nrays;
@@ -2675,7 +2681,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   if constexpr (PREFETCH_RS) rs_fetch(MW ? wv : 0);
   for (int a = MW ? wv : 0; a < A; a += MW ? nwv : 1) {
     int apos, ax, ay, ox, oy;
-    if (a < MFG_WAVE) {
+    if (!LR || a < MFG_WAVE) {
       apos = rl(agp, a);
       ax = rl(agx, a); ay = rl(agy, a);
       ox = rl(orgx, a); oy = rl(orgy, a);
@@ -2691,7 +2697,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
     for (int i = lane; i < S->fv_words; i += MFG_WAVE) fv[i] = 0xFFFFFFFFu;
     for (int i = lane; i < nsup4; i += MFG_WAVE) ((uint32_t*)wsup)[i] = 0u;
     for (int i = lane; i < ndsup; i += MFG_WAVE) dsup[i] = 0u;
-    for (int i = lane; i < 2 * S->lane_passes * dd; i += MFG_WAVE) amw[i] = 0u;
+    for (int i = lane; i < (wide ? 4 : 2) * dd; i += MFG_WAVE) amw[i] = 0u;
     if (has_dirt)
       for (int i = lane; i < dd; i += MFG_WAVE) wdirt[i] = 0u;
     tbl_sync<LR>();
@@ -2936,10 +2942,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // the cell-map read does not wait for the visibility read: its address is clamped on the bounds alone
       const uint32_t mraw = cmap_at<MM>(e, inb ? x * W + y : 0);
       const uint32_t m = v ? mraw : 0u;
-      const bool wall_sup = wsup[inwin ? wi : 0] != 0;
+      // CM_WALL | CM_DOOR when the cell's wall or door lost an identifier dedupe (a cell holds at most one of the two)
+      const uint32_t wall_sup = wsup[inwin ? wi : 0];
       // bit t = tag t (< 16) has a (not suppressed) entity here: the cell-map bits are the tag bits
-      // (wall_sup: the cell's wall or door lost an identifier dedupe; a cell holds at most one of the two)
-      uint32_t tags = m & ((wall_sup ? 0u : CM_WALL | CM_DOOR) | CM_ITEM | CM_POD | CM_DROP | CM_DIRT | CM_DEST);
+      uint32_t tags = (m & ~wall_sup) & (CM_WALL | CM_DOOR | CM_ITEM | CM_POD | CM_DROP | CM_DIRT | CM_DEST);
       if (MM) tags |= (m >> 1) & ((1u << MFG_TAG_MACHINES) | (1u << MFG_TAG_MAINTAINERS));
       // identifier-dedupe suppressions (rare): recompute the affected tags from the entity tables
       auto resup = [&](const int* tbl, int n, u64 sm, int tag, bool dest) {
@@ -2969,7 +2975,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
       // 0.4444 open, dirt = amount)
       auto tagv = [&](int tag) -> double {
-        if (tag >= MFG_TAG_AGENT0 + MFG_WAVE) {  // agents 64..127 (wide specs): the second mask table
+        if (wide && tag >= MFG_TAG_AGENT0 + MFG_WAVE) {  // agents 64..127: the second mask table
           const int b = tag - MFG_TAG_AGENT0 - MFG_WAVE;
           return (v && ((amw2[2 * wic + (b >> 5)] >> (b & 31)) & 1u)) ? 1.0 : 0.0;
         }
@@ -2999,7 +3005,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         const uint64_t ab = (uint64_t)(uint32_t)rl((int)lr_alo, l) | ((uint64_t)(uint32_t)rl((int)lr_ahi, l) << 32);
         int cnt = popc(tags & ut) + popc(amask & ab);
         if (wide) {  // agents 64..127: the layer's second agent word (uniform load) against the second mask table
-          const uint64_t ab2 = ((const MfgLayerRec CS*)S->lrec + (size_t)a * S->lmax + l)->agent_bits2;
+          const uint64_t ab2 = S->lrec_ab2[(size_t)a * S->lmax + l];
           const u64 am2 = v ? ((u64)amw2[2 * wic] | ((u64)amw2[2 * wic + 1] << 32)) : 0ull;
           cnt += popc(am2 & ab2);
         }
@@ -3087,13 +3093,13 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         const uint32_t ut = tf & 0xFFFFu, fl = tf >> 16;
         int cnt = popc(ct & ut) + popc(am & ab);
         if (wide) {  // agents 64..127: layer l's second agent word (per-lane load) against the second mask table
-          const uint64_t ab2 = ((const MfgLayerRec*)S->lrec + (size_t)a * S->lmax + l)->agent_bits2;
+          const uint64_t ab2 = S->lrec_ab2[(size_t)a * S->lmax + l];
           cnt += popc(((u64)amw2[2 * c] | ((u64)amw2[2 * c + 1] << 32)) & ab2);
         }
         OT out = (OT)cnt;  // a small count: exact in OT
         if (fl) {
           auto tagv = [&](int tag) -> double {
-            if (tag >= MFG_TAG_AGENT0 + MFG_WAVE) {  // agents 64..127 (wide specs): the second mask table
+            if (wide && tag >= MFG_TAG_AGENT0 + MFG_WAVE) {  // agents 64..127: the second mask table
               const int b = tag - MFG_TAG_AGENT0 - MFG_WAVE;
               return ((amw2[2 * c + (b >> 5)] >> (b & 31)) & 1u) ? 1.0 : 0.0;
             }
@@ -3415,10 +3421,12 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
     if (uni((int)S->rd_flag[env]) != 2) return;
   }
   Env e;
-  // MAINT, SEL 1: the step prefix, then the maintainer state and paths [o_mstate, o_grank) (16-B rounded) right
-  // after it instead of at their record offset (mdelta), then the count scratch: no MT, permutation or BFS scratch
+  // MAINT, SEL 1: the step prefix, then the maintainer states [o_mstate, o_mpath) (16-B rounded) right after it
+  // instead of at their record offset (mdelta), then the count scratch: no MT, permutation or BFS scratch. A step of
+  // these envs reads one cell of each maintainer's path (the one it advances to), in place in HBM: staging the whole
+  // paths (C5: 4 x 1,000 cells) was most of this launch's traffic (round 6)
   constexpr bool lm = MAINT && SEL == 1;
-  const int ms0 = S->L.o_mstate & ~15, mlen = lm ? ((S->L.o_grank + 15) & ~15) - ms0 : 0;
+  const int ms0 = S->L.o_mstate & ~15, mlen = lm ? ((S->L.o_mpath + 15) & ~15) - ms0 : 0;
   uint8_t* slice = smem + (size_t)wid * (lm ? S->L.o_logic + mlen + 4 * MFG_WAVE * NW : S->lds_logic);
   constexpr bool full = FULL && !lm;
   if (full) {
@@ -3426,7 +3434,10 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   } else {
     e.S = S; e.lds = slice; e.scratch = (int*)(slice + S->L.o_logic + mlen); e.stab = nullptr; e.cmap = nullptr;
     e.bfs = nullptr; e.hdrp = (int*)(slice + S->L.o_hdr); e.lane = lane_id();
-    if (lm) e.mdelta = S->L.o_logic - ms0;
+    if (lm) {
+      e.mdelta = S->L.o_logic - ms0;
+      e.gpath = (const uint16_t*)(state + (size_t)env * S->L.size + S->L.o_mpath);
+    }
   }
   uint8_t* rec = state + (size_t)env * S->L.size;
   // FULL without maintainers: a RespawnDirt rule is the only in-step reader of the MT state and the floor order, and
@@ -3443,7 +3454,8 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   // longer lean prefixes with dirt: only the live piles' slots (C2 / C4 / C5: 256 / 128 / 384 slots of 16 B). A lean
   // step never appends a pile (only RespawnDirt does, in the FULL instantiations), so the count it starts with bounds
   // every slot it reads or writes.
-  const bool trim = MFG_LOGIC_TRIM && !FULL && !one_pass && S->dirt_cap;
+  // (MAINT, SEL 1 too: its envs have no dirt spawn this step, so no pile is appended either)
+  const bool trim = MFG_LOGIC_TRIM && (!FULL || lm) && !one_pass && S->dirt_cap;
   const int nd0 = trim ? min(uni(((const int*)(rec + S->L.o_hdr))[H_N_DIRT]), S->dirt_cap) : 0;
   // the actions (a buffer load or Philox) while the record load is in flight
   const int A = S->A;
@@ -3510,7 +3522,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   if (lazy && rng_tail) rec_copy(rec + o_tail, e.lds + o_tail, n_tail, e.lane);
   // (lm: only the maintainer states go back; their paths are read-only here, since a maintainer whose path is used
   // up re-routes in the SEL 2 launch, and C5's 4 x 1,000-cell paths were most of k_logic's writes)
-  if constexpr (lm) rec_copy(rec + ms0, e.lds + S->L.o_logic, min(mlen, ((S->L.o_mpath + 15) & ~15) - ms0), e.lane);
+  if constexpr (lm) rec_copy(rec + ms0, e.lds + S->L.o_logic, mlen, e.lane);
 }
 #endif
 
