@@ -287,8 +287,6 @@ typedef struct mfg_variant {
                                  strides over several envs */
   int32_t serial;             /* 1: every kernel on the caller's stream in launch order (no resets or replay on the
                                  engine's second stream beside the render): per-kernel times for attribution */
-  int32_t reset_1wave;        /* 1: the one-wave auto-reset (k_resetdone) on specs that would take the two-wave one
-                                 (k_resetdone2: the reset's MT draws on a producer wave) */
 } mfg_variant;
 int mfg_create_variant(const mfg_spec* spec, int device, int64_t n_envs, const mfg_variant* variant,
                        mfg_engine** out);
@@ -335,8 +333,7 @@ int mfg_replay(mfg_engine* e, void* stream);
 
 /* Per-env state record layout (offsets) for host-side decoding, then the engine's launch facts (LDS slices,
  * o_logic, reset_overlap: 1 when a step's resets and their render run on the engine's second stream beside the
- * render of the other envs, reset_two_wave: 1 when auto-resets take the two-wave k_resetdone2); returns the number of
- * ints written (<= 64). */
+ * render of the other envs); returns the number of ints written (<= 64). */
 int mfg_layout(const mfg_engine* e, int32_t* out);
 void* mfg_state_ptr(mfg_engine* e);
 int64_t mfg_state_bytes(const mfg_engine* e);

@@ -140,10 +140,6 @@ struct MfgDevSpec {
   int32_t lds_replay_per_wave;  // k_replay slice: [hdr][MT + u16 perm image of the record][sink][tables]
   int32_t replay_mtperm, replay_sink_off, replay_stab_off, replay_stab_n;
   int32_t replay_top14;      // nf < 16384: shuffle draws use only the top 14 tempered bits (replay_shuffle_t)
-  // two-wave reset (k_resetdone2): the list lengths of a reset's MT-consuming shuffles in consumption order (SpawnAgents'
-  // floor shuffle and empty_positions draws per agent, then one floor shuffle per spawn rule); 0 entries: one-wave reset
-  int32_t reset_plan_n;
-  const uint16_t* reset_plan;
   // Combined obs layers whose members all encode 1.0 (walls, items, pods, drop-offs, destinations,
   // maintainers, agents) and appear once: the left-to-right f64 sum of 0/1 terms equals the member count,
   // so k_obs places popc(tags & comb_unit_tags) + popc(agents & comb_agents) instead of a member loop

@@ -33,8 +33,6 @@ struct mfg_engine {
   bool replay_each = false; // pay the shuffle debt after every step, not once per call (long resets + in-step RNG)
   int obs_nwv = 1;          // waves per env of the render (> 1: multi-wave render, k_obs_mw)
   bool replay2 = false;     // two-wave replay (k_replay2) for floor lists whose 1-wave slice fills a SIMD
-  bool reset2 = false;      // two-wave auto-reset (k_resetdone2): the spec has a reset plan
-  int rd2_blocks = 1;       // k_resetdone2 workgroups (two waves each)
   struct Mark { int k; hipEvent_t a, b; };
   std::vector<Mark> marks;
   std::string err;  // mfg_last_error(e)
@@ -332,7 +330,7 @@ extern "C" int mfg_create_variant(const mfg_spec* s, int device, int64_t n_envs,
   if (!s || !out) return fail("null argument");
   if (n_envs < 1) return fail("n_envs must be >= 1");
   if (validate_spec(s)) return -1;
-  const mfg_variant none{0, 0, 0, 0, 0, 0, 0};
+  const mfg_variant none{0, 0, 0, 0, 0, 0};
   DevGuard g(device);
   return create_impl(s, device, n_envs, v ? *v : none, out);
 }
@@ -495,38 +493,6 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
     h.replay_top14 = h.nf < 16384 && !v.full_temper;  // (mfg_variant.full_temper: that path on small levels)
   }
   pcg64_seed(s->env_seed, &h.pcg_init_hi, &h.pcg_init_lo, &h.pcg_inc_hi, &h.pcg_inc_lo);
-  // the two-wave reset's plan (k_resetdone2, mfg_kernels.h ring_next): the list lengths of the reset's MT draws in
-  // env_reset's order, when none depends on the state: per agent (SpawnAgents, rules.py:182-199) the floor shuffle and
-  // the draws of shuffle(empty_positions) (nf - nd - a cells), then one floor shuffle per spawn rule that draws
-  // positions. Configured agent positions (one more shuffle only if a cell is free), SpawnDestinationsPerAgent and
-  // DoRandomInitialSteps (draws over state-dependent lists) keep the one-wave reset.
-  std::vector<uint16_t> plan;
-  {
-    bool ok = !v.reset_1wave && h.xchg_ordered && s->n_floor >= 2;
-    for (int a = 0; a < s->n_agents && ok; a++) {
-      if (s->n_positions[a] > 0) ok = false;
-      plan.push_back((uint16_t)s->n_floor);
-      const int m = s->n_floor - s->n_doors - a;
-      if (m >= 2) plan.push_back((uint16_t)m);
-    }
-    for (int r = 0; r < s->n_rules && ok; r++) {
-      const mfg_rule& ru = s->rules[r];
-      switch (ru.op) {
-        case MFG_RULE_SPAWN_PODS: case MFG_RULE_SPAWN_DROPOFFS: case MFG_RULE_SPAWN_ITEMS: case MFG_RULE_SPAWN_DESTS:
-          if (ru.i[0] > 0) plan.push_back((uint16_t)s->n_floor);
-          break;
-        case MFG_RULE_SPAWN_DIRT: case MFG_RULE_SPAWN_MACHINES: case MFG_RULE_SPAWN_MAINTAINERS:
-          plan.push_back((uint16_t)s->n_floor);
-          break;
-        case MFG_RULE_SPAWN_DEST_PER_AGENT: ok = false; break;
-        case MFG_RULE_RANDOM_INIT_STEPS: if (ru.i[0] > 0) ok = false; break;
-        default: break;
-      }
-    }
-    if (!ok || h.lds_full + RR_RING > MFG_LDS_MAX) plan.clear();
-  }
-  h.reset_plan_n = (int)plan.size();
-  h.reset_plan = nullptr;
   // static tables
   std::vector<uint8_t> door_of(HW, 0xFF);
   for (int d = 0; d < s->n_doors; d++) door_of[s->door_cells[d]] = (uint8_t)d;
@@ -673,7 +639,6 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   }
   rc |= upload(e, node_ok.data(), node_ok.size(), &h.node_ok);
   rc |= upload(e, wd.data(), wd.size(), &h.wd_pairs);
-  rc |= upload(e, plan.data(), plan.size(), &h.reset_plan);
   if (rc) { delete e; return -1; }
   if (hipMalloc((void**)&e->d_spec, sizeof(MfgDevSpec)) != hipSuccess ||
       hipMemcpy(e->d_spec, &h, sizeof(MfgDevSpec), hipMemcpyHostToDevice) != hipSuccess) {
@@ -749,18 +714,6 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
       delete e; return fail("occupancy query failed");
     }
     e->rd_blocks = std::max(1, per_cu) * std::max(1, n_cu);
-#ifndef MFG_RESET2
-#define MFG_RESET2 1  // 0: the one-wave auto-reset for every spec (A/B timing)
-#endif
-    e->reset2 = MFG_RESET2 && h.reset_plan_n > 0;
-    if (e->reset2) {
-      const size_t lds2 = (size_t)h.lds_full + RR_RING;
-      const hipError_t occ2 = h.lane_passes == 2
-                                  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resetdone2<2>, 2 * MFG_WAVE, lds2)
-                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resetdone2<1>, 2 * MFG_WAVE, lds2);
-      if (occ2 != hipSuccess) { delete e; return fail("occupancy query failed"); }
-      e->rd2_blocks = std::max(1, per_cu) * std::max(1, n_cu);
-    }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_replay_done, 64, (size_t)h.lds_replay_per_wave) !=
         hipSuccess) {
       delete e; return fail("occupancy query failed");
@@ -843,7 +796,7 @@ extern "C" int mfg_layout(const mfg_engine* e, int32_t* out) {
                        e->h.lmax, e->h.obs_agent_stride, e->h.lds_full, e->h.xchg_ordered, L.o_machines,
                        L.o_maints, L.o_mstate, L.o_mpath, L.o_grank, e->h.dirt_cap, e->h.lds_logic, e->h.lds_obs,
                        e->h.lds_replay_per_wave, e->h.bfs_off, e->h.bfs_bytes, e->h.max_pairs, e->h.scratch_bytes,
-                       L.o_logic, e->overlap ? 1 : 0, e->reset2 ? 1 : 0};
+                       L.o_logic, e->overlap ? 1 : 0};
   const int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
@@ -1126,16 +1079,7 @@ static int step_impl(mfg_engine* e, int K, const int32_t* actions, uint32_t phil
                          (size_t)e->h.lds_replay_per_wave, rs, e->d_spec, e->d_state, (long long)e->B, rd_cur);
       const int wpb = wpb_for(e->h.lds_full);
       const long long nwg = std::min<long long>(env_grid(e, wpb), e->rd_blocks);
-      if (e->reset2) {  // one env per two-wave workgroup: a producer of the reset's draws beside Factory.reset()
-        const long long nwg2 = std::min<long long>(e->B, e->rd2_blocks);
-        const size_t lds2 = (size_t)e->h.lds_full + RR_RING;
-        if (e->h.lane_passes == 2)
-          hipLaunchKernelGGL(k_resetdone2<2>, dim3((unsigned)nwg2), dim3(2 * MFG_WAVE), lds2, rs, e->d_spec,
-                             e->d_state, (long long)e->B, rd_cur);
-        else
-          hipLaunchKernelGGL(k_resetdone2<1>, dim3((unsigned)nwg2), dim3(2 * MFG_WAVE), lds2, rs, e->d_spec,
-                             e->d_state, (long long)e->B, rd_cur);
-      } else if (e->h.lane_passes == 2)
+      if (e->h.lane_passes == 2)
         hipLaunchKernelGGL(k_resetdone<2>, dim3((unsigned)nwg), dim3(wpb * 64), (size_t)e->h.lds_full * wpb, rs,
                            e->d_spec, e->d_state, (long long)e->B, rd_cur);
       else

@@ -88,8 +88,6 @@ struct Env {
   int lane;
   int mdelta = 0;   // where the maintainer states sit relative to their record offset (k_logic<.., SEL 1>)
   const uint16_t* gpath = nullptr;  // k_logic<.., SEL 1>: the maintainer paths read in place in the HBM record
-  uint8_t* ring = nullptr;  // two-wave reset (k_resetdone2), consumer wave: the producer's chunk ring (draws from LDS)
-  int* rctl = nullptr;      // ... and its control words (RR_*)
   __device__ int* hdr() const { return hdrp; }
   __device__ int* rctr() const { return (int*)(lds + S->L.o_rule_ctr); }
   __device__ int* agpos() const { return (int*)(lds + S->L.o_agent_pos); }
@@ -559,10 +557,8 @@ struct Rp2Prod {  // producer state carried across ring phases
   int s, icur, idx;
   uint32_t yw;
 };
-// The producer half of RP2_R chunks: d shuffles, shuffle s of hi_of(s) + 1 elements (the replay: every shuffle is the
-// floor list; the two-wave reset: the reset's shuffle plan, MfgDevSpec::reset_plan)
-template <bool TOP14, typename HiF>
-__device__ __forceinline__ void rp2_produce_f(const Env& e, uint8_t* half, int* cnt, Rp2Prod& st, int d, HiF hi_of) {
+template <bool TOP14>
+__device__ void rp2_produce(const Env& e, uint8_t* half, int* cnt, Rp2Prod& st, int d, int hi) {
   uint32_t* mt = e.mt();
   const int lane = e.lane, lo = 1;
   int n = 0;
@@ -601,23 +597,23 @@ __device__ __forceinline__ void rp2_produce_f(const Env& e, uint8_t* half, int* 
     n++;
     if (st.icur < lo) {  // this shuffle is done: the next one starts at the top
       st.s++;
-      st.icur = hi_of(st.s);
+      st.icur = hi;
     }
   }
   if (lane == 0) *cnt = n;
 }
-template <bool TOP14>
-__device__ void rp2_produce(const Env& e, uint8_t* half, int* cnt, Rp2Prod& st, int d, int hi) {
-  rp2_produce_f<TOP14>(e, half, cnt, st, d, [hi](int) { return hi; });
-}
-// The swap block of one chunk record (icur, nacc >= 1, the accepted draws' j in rank order) applied to perm, lane = rank
-// (the consumer half of replay_shuffle_t)
-__device__ __forceinline__ void rp2_apply_chunk(const Env& e, uint16_t* perm, const uint8_t* rec, int icur, int nacc,
-                                                uint32_t& ctr) {
+__device__ void rp2_consume(const Env& e, const uint8_t* half, int n, uint32_t& ctr) {
+  uint16_t* perm = e.perm();
   const int lane = e.lane;
   uint16_t* sink = (uint16_t*)e.scratch + lane;
   uint32_t* ptab = e.stab;
-  {
+  // the half's chunk headers, lane q = chunk q (read per chunk with v_readlane, off the LDS chain)
+  const int hds = lane < n ? *(const int*)(half + lane * RP2_REC) : 0;
+  for (int q = 0; q < n; q++) {
+    const uint8_t* rec = half + q * RP2_REC;
+    const int hd = rl(hds, q);
+    const int icur = hd & 0xFFFF, nacc = hd >> 16;
+    if (!nacc) continue;
     const bool acc = lane < nacc;
     const int A = lane;
     // j and the value leaving i are read together (one LDS round trip)
@@ -660,105 +656,11 @@ __device__ __forceinline__ void rp2_apply_chunk(const Env& e, uint16_t* perm, co
     wave_sync();
   }
 }
-__device__ void rp2_consume(const Env& e, const uint8_t* half, int n, uint32_t& ctr) {
-  uint16_t* perm = e.perm();
-  const int lane = e.lane;
-  // the half's chunk headers, lane q = chunk q (read per chunk with v_readlane, off the LDS chain)
-  const int hds = lane < n ? *(const int*)(half + lane * RP2_REC) : 0;
-  for (int q = 0; q < n; q++) {
-    const int hd = rl(hds, q);
-    const int icur = hd & 0xFFFF, nacc = hd >> 16;
-    if (nacc) rp2_apply_chunk(e, perm, half + q * RP2_REC, icur, nacc, ctr);
-  }
-}
-
-// ---- two-wave reset (k_resetdone2): the reset's MT draws on a producer wave --------------------------------------
-// A reset's floor shuffles (SpawnAgents, the spawn rules, the finishing env's debt) and SpawnAgents' draws-only shuffles
-// of empty_positions consume the MT stream in an order and with list lengths fixed by the spec (MfgDevSpec::reset_plan,
-// built by mfg_create; specs whose reset draws depend on the state keep the one-wave reset). So a producer wave runs
-// all of a reset's draws ahead into the k_replay2 chunk ring while the consumer wave runs env_reset and takes each
-// shuffle's chunks from the ring: the swap blocks (rp2_apply_chunk) or, for empty_positions, the first accepted draw.
-// The waves meet at one workgroup barrier per ring half; the consumer asks for the next half when it has used its
-// half up, the producer fills one half per barrier and leaves after the barrier at which the consumer is done.
-#define RR_RING (2 * RP2_R * RP2_REC + 32)  // both halves + 8 control words
-enum { RR_DONE = 2, RR_PHASE, RR_POS, RR_BAD };  // control words after the two half counts
-// The consumer's place in the ring, in registers for the length of one shuffle (loaded from and stored back to the
-// control words once per shuffle); hds: the current half's chunk headers, lane q = chunk q.
-struct RingPos {
-  int phase, pos, n, hds;
-};
-__device__ __forceinline__ const uint8_t* ring_half(const Env& e, int phase) {
-  return e.ring + ((phase - 1) & 1) * RP2_R * RP2_REC;
-}
-__device__ __forceinline__ RingPos ring_load(const Env& e) {
-  const int* ctl = e.rctl;
-  RingPos rp;
-  rp.phase = uni(ctl[RR_PHASE]);
-  rp.pos = uni(ctl[RR_POS]);
-  rp.n = rp.phase ? uni(ctl[(rp.phase - 1) & 1]) : 0;
-  rp.hds = rp.phase && e.lane < rp.n ? *(const int*)(ring_half(e, rp.phase) + e.lane * RP2_REC) : 0;
-  return rp;
-}
-__device__ __forceinline__ void ring_store(const Env& e, const RingPos& rp) {
-  wave_sync();
-  if (e.lane == 0) { e.rctl[RR_PHASE] = rp.phase; e.rctl[RR_POS] = rp.pos; }
-  wave_sync();
-}
-// the next chunk (false: the plan ran out, which a spec mfg_create admits cannot do: the env is flagged)
-__device__ __forceinline__ bool ring_advance(const Env& e, RingPos& rp) {
-  if (rp.pos < rp.n) return true;
-  if (uni(e.rctl[RR_BAD])) return false;
-  __syncthreads();  // this half is used up: the producer has filled the other one by this barrier
-  rp.phase++;
-  rp.pos = 0;
-  rp.n = uni(e.rctl[(rp.phase - 1) & 1]);
-  if (rp.n == 0) {
-    wave_sync();
-    if (e.lane == 0) { e.rctl[RR_BAD] = 1; e.hdrp[H_OVERFLOW] = 1; }  // the next step reports a capacity crash
-    wave_sync();
-    return false;
-  }
-  rp.hds = e.lane < rp.n ? *(const int*)(ring_half(e, rp.phase) + e.lane * RP2_REC) : 0;
-  return true;
-}
-// one floor shuffle (swap blocks) from the ring
-__device__ void ring_shuffle(const Env& e, uint16_t* perm) {
-  uint32_t ctr = (uint32_t)uni((int)e.stab[RP_CTR]);
-  RingPos rp = ring_load(e);
-  while (ring_advance(e, rp)) {
-    const int hd = rl(rp.hds, rp.pos);
-    const int icur = hd & 0xFFFF, nacc = hd >> 16;
-    if (nacc) rp2_apply_chunk(e, perm, ring_half(e, rp.phase) + rp.pos * RP2_REC, icur, nacc, ctr);
-    rp.pos++;
-    if (icur - nacc < 1) break;
-  }
-  ring_store(e, rp);
-  if (e.lane == 0) e.stab[RP_CTR] = ctr;
-  wave_sync();
-}
-// one draws-only shuffle from the ring: j of its first accepted draw (replay_shuffle_t<.., false>)
-__device__ int ring_first_j(const Env& e) {
-  int fj = -1;
-  RingPos rp = ring_load(e);
-  while (ring_advance(e, rp)) {
-    const int hd = rl(rp.hds, rp.pos);
-    const int icur = hd & 0xFFFF, nacc = hd >> 16;
-    if (fj < 0 && nacc) fj = uni((int)((const uint16_t*)(ring_half(e, rp.phase) + rp.pos * RP2_REC + 4))[0]);
-    rp.pos++;
-    if (icur - nacc < 1) break;
-  }
-  ring_store(e, rp);
-  return fj;
-}
 
 // random.shuffle(Entities._floor_positions) (global_entities.py:47-55)
 template <typename PT>
 __device__ __forceinline__ void floor_shuffle_t(const Env& e, PT* perm) {
   if constexpr (sizeof(PT) == 2) {
-    if (e.ring) {  // two-wave reset: the draws come from the producer wave
-      ring_shuffle(e, perm);
-      return;
-    }
     if (e.S->xchg_ordered) {  // the branch-free exchange path (the replay kernel's) whenever it is probed
       replay_shuffle(e, perm);
       return;
@@ -2203,9 +2105,8 @@ __device__ __attribute__((always_inline)) void env_reset(const Env& e, int* scra
     // the draws of shuffle(empty_positions) on the replay's branch-free chunked path; the first accepted draw
     // (i = m - 1) picks the slot pop() takes
     const int j = m < 2 ? (m == 1 ? 0 : -1)
-                        : (e.ring ? ring_first_j(e)
-                                  : (S->replay_top14 ? replay_shuffle_t<true, false>(e, nullptr, m - 1)
-                                                     : replay_shuffle_t<false, false>(e, nullptr, m - 1)));
+                        : (S->replay_top14 ? replay_shuffle_t<true, false>(e, nullptr, m - 1)
+                                           : replay_shuffle_t<false, false>(e, nullptr, m - 1));
     int k = 0, cell = -1;
     const int npos = S->s.n_positions[a];
     if (npos > 0) {
@@ -3652,85 +3553,6 @@ k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B, int rd_slot) {
     wave_sync();
     rec_copy(rec, e.lds, S->L.size, e.lane);
     wave_sync();
-  }
-}
-#endif
-
-// The producer wave of one two-wave reset: the finishing env's debt (floor shuffles, none after k_replay_done) and the
-// spec's reset plan, into the chunk ring, one half per barrier; it leaves after the barrier at which the consumer is done
-template <bool TOP14>
-__device__ void ring_produce(const Env& e, uint8_t* ring, int* ctl, int debt) {
-  SpecP S = e.S;
-  const int nf = S->nf, d = debt + S->reset_plan_n;
-  auto hi_of = [&](int s) { return (s < debt ? nf : (s < d ? (int)S->reset_plan[s - debt] : 2)) - 1; };
-  Rp2Prod st;
-  st.s = 0;
-  st.icur = hi_of(0);
-  st.idx = e.H(H_MT_IDX);
-  st.yw = st.idx <= 560 ? e.mt()[st.idx + e.lane] : 0u;
-  bool fin = false;
-  auto finish = [&]() {  // every draw made: the MT state canonical (CPython's mti), as replay_shuffle_t leaves it
-    int idx = st.idx;
-    if (idx > 624) {
-      mt_twist(e);
-      idx -= 624;
-    }
-    e.setH(H_MT_IDX, idx);
-    wave_sync();
-    fin = true;
-  };
-  if (d > 0) rp2_produce_f<TOP14>(e, ring, &ctl[0], st, d, hi_of);
-  else if (e.lane == 0) ctl[0] = 0;
-  if (st.s >= d) finish();
-  for (int phase = 1;; phase++) {
-    __syncthreads();
-    if (uni(ctl[RR_DONE])) break;
-    if (st.s < d) rp2_produce_f<TOP14>(e, ring + (phase & 1) * RP2_R * RP2_REC, &ctl[phase & 1], st, d, hi_of);
-    else if (e.lane == 0) ctl[phase & 1] = 0;
-    if (st.s >= d && !fin) finish();
-  }
-}
-
-// Two-wave auto-reset of the envs on a step's done list (specs with a reset plan, see ring_load): wave 1 produces the
-// reset's draws, wave 0 runs Factory.reset() on the record image; one env per workgroup at a time, a resident grid
-// striding over the list. Results are those of k_resetdone (same draws, same swaps, same order).
-#ifndef MFG_OBS_UNIT  // host-unit kernel (not compiled in the render units)
-template <int NW>
-static __global__ void __launch_bounds__(2 * MFG_WAVE) k_resetdone2(const MfgDevSpec* S_, uint8_t* state, long long B,
-                                                                    int rd_slot) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  SpecP S = (SpecP)S_;
-  const int wv = uni(threadIdx.x >> 6);
-  const int32_t* lst = S->rd_list + (size_t)rd_slot * (size_t)(B + 2);
-  const long long n = min((long long)uni(lst[0]), B);
-  uint8_t* ring = smem + S->lds_full;
-  int* ctl = (int*)(ring + 2 * RP2_R * RP2_REC);
-  for (long long q = blockIdx.x; q < n; q += gridDim.x) {
-    const long long env = uni(lst[2 + q]);
-    if (env < 0 || env >= B) continue;
-    uint8_t* rec = state + (size_t)env * S->L.size;
-    if (uni(((const int*)(rec + S->L.o_hdr))[H_DONE]) == 0) continue;
-    Env e;
-    env_full(S, smem, e, env);
-    const int t = wv * MFG_WAVE + e.lane, n16 = S->L.size >> 4;
-    for (int i = t; i < n16; i += 2 * MFG_WAVE) ((uint4*)e.lds)[i] = ((const uint4*)rec)[i];
-    if (wv == 0 && e.lane < 8) ctl[e.lane] = 0;
-    __syncthreads();
-    if (wv == 1) {
-      const int debt = e.H(H_DEBT);
-      if (S->replay_top14) ring_produce<true>(e, ring, ctl, debt);
-      else ring_produce<false>(e, ring, ctl, debt);
-    } else {
-      e.ring = ring;
-      e.rctl = ctl;
-      env_reset<NW>(e, e.scratch);
-      e.setH(H_DONE, 0);
-      wave_sync();
-      if (e.lane == 0) ctl[RR_DONE] = 1;
-      __syncthreads();  // pairs with the producer's last barrier
-    }
-    for (int i = t; i < n16; i += 2 * MFG_WAVE) ((uint4*)rec)[i] = ((const uint4*)e.lds)[i];
-    __syncthreads();  // the slice is free for the next env
   }
 }
 #endif

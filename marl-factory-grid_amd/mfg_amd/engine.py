@@ -22,7 +22,7 @@ LAYOUT_KEYS = ['size', 'o_hdr', 'o_rule_ctr', 'o_agent_pos', 'o_agent_arr', 'o_a
                'o_battery', 'o_frozen_bat', 'o_dirt_amt', 'o_pcg', 'o_mt', 'o_perm', 'lmax', 'obs_agent_stride',
                'lds_full', 'xchg_ordered', 'o_machines', 'o_maints', 'o_mstate', 'o_mpath', 'o_grank', 'dirt_cap',
                'lds_logic', 'lds_obs', 'lds_replay', 'bfs_off', 'bfs_bytes', 'max_pairs', 'scratch_bytes', 'o_logic',
-               'reset_overlap', 'reset_two_wave']
+               'reset_overlap']
 # header slots (csrc/mfg_device.h)
 HDR = {k: i for i, k in enumerate([
     'step', 'episode', 'crashed', 'frozen', 'obs_init', 'debt', 'mt_idx', 'n_items', 'n_pods', 'n_drops',
@@ -103,7 +103,7 @@ class MfgVariant(C.Structure):
     """include/mfg.h mfg_variant: exact alternative code paths forced for the parity tests."""
     _fields_ = [('shuffle_table_path', C.c_int32), ('full_temper', C.c_int32), ('bfs_hbm', C.c_int32),
                 ('pairs_lds', C.c_int32), ('render_slots', C.c_int32),
-                ('serial', C.c_int32), ('reset_1wave', C.c_int32)]
+                ('serial', C.c_int32)]
 
 
 class Engine:
