@@ -121,8 +121,7 @@ struct MfgDevSpec {
   int32_t lds_obs;           // k_obs: lean record + cell map + id-collision pairs + first-visit table + wall sup
   int32_t lds_obs_shared;    // the env-wide part of it (lean record, cell map, pairs; 16-B aligned)
   int32_t lds_obs_wave;      // the per-agent tables (multi-wave render: one copy per wave after the shared part)
-  int32_t fv_words;          // first-visit table entries ((2d+1) rows of fv_stride, rounded up to 4)
-  int32_t fv_stride;         // first-visit table row stride: 2d+1, or padded (MFG_FV_PAD) against LDS bank conflicts
+  int32_t fv_words;          // first-visit table entries ((2d+1)^2, rounded up to 4)
   int32_t mmax, kmax;        // machines / maintainers per env (spawn quantities)
   int32_t mstate_ints, path_cap;  // ints per maintainer state; max stored path length (cells)
   int32_t bfs_off;           // offset of the BFS scratch in the full-record LDS slice (0 = none or in HBM)

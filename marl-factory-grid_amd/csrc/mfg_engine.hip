@@ -156,62 +156,6 @@ static void pcg64_seed(uint32_t entropy, uint64_t* st_hi, uint64_t* st_lo, uint6
 
 static int align_up(int x, int a) { return (x + a - 1) / a * a; }
 
-#ifndef MFG_FV_PAD
-#define MFG_FV_PAD 0  // 1: pad the first-visit table's rows against LDS bank conflicts (fv_stride_for)
-#endif
-// Row stride of the render's first-visit table ((2 fr + 1) rows around the ray origin). With MFG_FV_PAD the stride in
-// [2 fr + 1, 2 fr + 33) with the fewest LDS bank conflicts (dword banks mod 32 per 32-lane half, distinct addresses;
-// identical ones broadcast) over the two per-agent access patterns: the placement's read of the window cells (lane =
-// window cell) and the ray walk's first-visit atomics (lane = ray, one instruction per ray point).
-static int fv_stride_for(const mfg_spec* s, const MfgDevSpec& h) {
-  const int fw = 2 * h.fr + 1;
-  if (!MFG_FV_PAD) return fw;
-  auto group_cost = [](const std::vector<int>& addr) {  // extra LDS cycles of one 64-lane access
-    int cost = 0;
-    for (int g = 0; g < 2; g++) {
-      std::vector<std::vector<int>> bank(32);
-      for (int l = 32 * g; l < 32 * g + 32 && l < (int)addr.size(); l++) {
-        if (addr[l] < 0) continue;
-        auto& b = bank[addr[l] & 31];
-        if (std::find(b.begin(), b.end(), addr[l]) == b.end()) b.push_back(addr[l]);
-      }
-      int mx = 1;
-      for (auto& b : bank) mx = std::max(mx, (int)b.size());
-      cost += mx - 1;
-    }
-    return cost;
-  };
-  int best = fw, best_cost = INT32_MAX;
-  for (int fws = fw; fws < fw + 32; fws++) {
-    int cost = 0;
-    // placement: window cell wi of the (oh x ow) window at a fixed offset inside the table
-    for (int w0 = 0; w0 < h.dd; w0 += 64) {
-      std::vector<int> a(64);
-      for (int l = 0; l < 64; l++) {
-        const int wi = std::min(w0 + l, h.dd - 1);
-        a[l] = (wi / h.ow) * fws + wi % h.ow;
-      }
-      cost += group_cost(a);
-    }
-    // ray walk: point p of every ray of a 64-ray pass
-    for (int r0 = 0; r0 < s->n_rays; r0 += 64) {
-      int maxlen = 0;
-      for (int r = r0; r < std::min(r0 + 64, s->n_rays); r++) maxlen = std::max(maxlen, s->ray_off[r + 1] - s->ray_off[r]);
-      for (int p = 1; p < maxlen; p++) {
-        std::vector<int> a(64, -1);
-        for (int r = r0; r < std::min(r0 + 64, s->n_rays); r++)
-          if (p < s->ray_off[r + 1] - s->ray_off[r]) {
-            const int q = s->ray_off[r] + p;
-            a[r - r0] = (s->ray_pts[2 * q] + h.fr) * fws + s->ray_pts[2 * q + 1] + h.fr;
-          }
-        cost += group_cost(a);
-      }
-    }
-    if (cost < best_cost) { best_cost = cost; best = fws; }
-  }
-  return best;
-}
-
 static void make_layout(const mfg_spec* s, MfgLayout* L, int imax, int pmax, int dropmax, int destmax, int mmax,
                         int kmax, int mstate_ints, int path_cap, int graph, int dirt_cap) {
   // [0, o_logic): what a step reads and writes (k_logic stages only this prefix); [o_logic, o_mt): the
@@ -531,8 +475,7 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   }
   h.pair_pool = nullptr;
   h.lds_logic = h.step_rng ? h.lds_full : h.L.o_logic + 4 * MFG_WAVE * h.lane_passes;  // step prefix + per-door count scratch
-  h.fv_stride = fv_stride_for(s, h);
-  h.fv_words = align_up((2 * h.fr + 1) * h.fv_stride, 4);
+  h.fv_words = align_up((2 * h.fr + 1) * (2 * h.fr + 1), 4);
   h.lds_obs = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) +
               4 * h.fv_words + align_up(h.dd, 16) + 4 * MFG_WAVE + h.dirt_cap / 8 +
               8 * (s->n_agents > MFG_WAVE ? 2 : 1) * h.dd +  // + per-window-cell agent masks (u64 per 64 agents)
@@ -582,9 +525,6 @@ static int create_impl(const mfg_spec* s, int device, int64_t n_envs, const mfg_
   // LDS holds up to MFG_PAIRS_LDS pairs (the usual case); the bound's remainder spills to an HBM pool
   h.pairs_lds = std::min(h.max_pairs, MFG_PAIRS_LDS);
   if (v.pairs_lds > 0) h.pairs_lds = std::max(1, std::min(h.pairs_lds, (int)v.pairs_lds));  // mfg_variant
-  // an even count: the 12-B pairs then end 8-B aligned, and so do the render's per-agent tables after them (its
-  // 64-bit agent-mask reads); a slot past max_pairs is never used
-  h.pairs_lds += h.pairs_lds & 1;
   h.lds_obs += 12 * h.pairs_lds;
   h.lds_obs_shared = align_up(h.L.o_mt, 16) + ((h.mmax || h.kmax) ? h.map_bytes : h.map_bytes8) + 12 * h.pairs_lds;
   h.lds_obs_wave = align_up(h.lds_obs - h.lds_obs_shared, 16);

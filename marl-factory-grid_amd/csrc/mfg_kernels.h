@@ -2503,12 +2503,9 @@ __device__ int build_id_pairs(const Env& e, const PairList& pairs) {
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) u64 lds_u64;
 // the render's per-agent tables: LDS, or (long-ray render, k_obs_lr) the wave's HBM pool slot
 template <bool LR>
 using obs_u32 = typename std::conditional<LR, uint32_t, lds_u32>::type;
-template <bool LR>
-using obs_u64 = typename std::conditional<LR, u64, lds_u64>::type;
 template <typename DP>
 struct SupT {  // per-agent suppression sets from the identifier dedupe
   u64 items, pods, drops, dests, machines, maints;
@@ -2567,9 +2564,6 @@ struct ObsPacked {
 #ifndef MFG_OBS_FLAT_PK
 #define MFG_OBS_FLAT_PK 1  // packed renders with wide windows queue their entries from the flattened pass too
 #endif
-#ifndef MFG_OBS_SEL2
-#define MFG_OBS_SEL2 0  // flattened pass: door and battery layer values by selects instead of the flag branch
-#endif
 #define CT_CLOSED 0x80000000u  // stashed tag word: the door on the cell is closed (tags stay below bit 16)
 __device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
@@ -2593,7 +2587,6 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   constexpr bool LR = MAXPTS == 0;
   constexpr int RMP = LR ? 2 : MAXPTS;  // RayLane width (unused by the long-ray walk)
   typedef obs_u32<LR> tu32;
-  typedef obs_u64<LR> tu64;  // the agent-mask table read and written as whole 64-bit cells (amw is 8-B aligned)
   // window: oh x ow cells from (wx0, wy0) = agent - r, or the whole level at (0, 0) when pomdp_r == 0
   // (observation_builder.py:152-158); rays and the first-visit table have radius fr (Q13)
   const int A = S->A, H = S->s.H, W = S->s.W, oh = S->oh, ow = S->ow, dd = S->dd, fr = S->fr;
@@ -2625,7 +2618,6 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
   uint32_t* fv = LR ? (uint32_t*)(S->obs_pool + (size_t)slot * (size_t)S->obs_slot_bytes)
                     : (uint32_t*)(e.scratch + 3 * S->pairs_lds + (MW ? wv * (S->lds_obs_wave >> 2) : 0));
   const int fw = 2 * fr + 1;
-  const int fws = S->fv_stride;  // row stride of the first-visit table (>= fw; padded against LDS bank conflicts)
   uint8_t* wsup = (uint8_t*)(fv + S->fv_words);  // [dd] window cells whose wall or door the dedupe suppressed
   const int nsup4 = (dd + 3) >> 2;
   // dirt suppression bitmap for groups wider than a wave: after the per-lane sink words of the ray walk
@@ -2762,7 +2754,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
           for (int q = 0; q < 32; q++) {
             const int dx = (int)(int16_t)(pt[q] & 0xFFFFu), dy = (int)(int16_t)(pt[q] >> 16);
             const bool vq = ((vism >> q) & 1u) && (s0 + q > 0);  // the origin (point 0) is stored once below
-            atomicMin(vq ? &fv[(dx + fr) * fws + dy + fr] : sink, (uint32_t)((ray_id << 8) + s0 + q));
+            atomicMin(vq ? &fv[(dx + fr) * fw + dy + fr] : sink, (uint32_t)((ray_id << 8) + s0 + q));
           }
         }
       }
@@ -2829,10 +2821,10 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       // ray 0's rank 0, stored once below instead of a 64-lane same-address atomic
 #pragma unroll
       for (int p = 1; p < RMP; p++)
-        atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + fr) * fws + ray.dy(p) + fr] : sink,
+        atomicMin(((vism >> p) & 1u) ? &fv[(ray.dx(p) + fr) * fw + ray.dy(p) + fr] : sink,
                   (uint32_t)((ray_id << RayLane<RMP>::RSH) + p));
     }
-    if (lane == 0) fv[fr * fws + fr] = 0u;
+    if (lane == 0) fv[fr * fw + fr] = 0u;
     tbl_sync<LR>();
     // ---- identifier dedupe: of two visible entities with equal identifiers the later first visit loses
     SupT<tu32> sup;
@@ -2849,7 +2841,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       const int xB = (pB >> 16) - ox + fr, yB = (pB & 0xFFFF) - oy + fr;
       const bool nearq = (q < npairs) & ((unsigned)xA < (unsigned)fw) & ((unsigned)yA < (unsigned)fw) &
                          ((unsigned)xB < (unsigned)fw) & ((unsigned)yB < (unsigned)fw);
-      const uint32_t rA0 = fv[nearq ? xA * fws + yA : 0], rB0 = fv[nearq ? xB * fws + yB : 0];
+      const uint32_t rA0 = fv[nearq ? xA * fw + yA : 0], rB0 = fv[nearq ? xB * fw + yB : 0];
       const uint32_t rA = nearq ? rA0 : 0xFFFFFFFFu, rB = nearq ? rB0 : 0xFFFFFFFFu;
       u64 hm = ballot(rA != 0xFFFFFFFFu && rB != 0xFFFFFFFFu);
       while (hm) {
@@ -2945,7 +2937,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       const int lx = x - ox + fr, ly = y - oy + fr;
       const bool inb = inwin & ((unsigned)x < (unsigned)H) & ((unsigned)y < (unsigned)W) &
                        ((unsigned)lx < (unsigned)fw) & ((unsigned)ly < (unsigned)fw);
-      const bool v = inb & (fv[inb ? lx * fws + ly : 0] != 0xFFFFFFFFu);
+      const bool v = inb & (fv[inb ? lx * fw + ly : 0] != 0xFFFFFFFFu);
       const int cell = v ? x * W + y : 0;
       // the cell-map read does not wait for the visibility read: its address is clamped on the bounds alone
       const uint32_t mraw = cmap_at<MM>(e, inb ? x * W + y : 0);
@@ -2978,7 +2970,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
         tags = di ? (tags | (1u << MFG_TAG_DIRT)) : (tags & ~(1u << MFG_TAG_DIRT));
       }
       const int wic = inwin ? wi : 0;
-      const u64 amraw = ((const tu64*)amw)[wic];
+      const u64 amraw = (u64)amw[2 * wic] | ((u64)amw[2 * wic + 1] << 32);
       const u64 amask = v ? amraw : 0ull;
       // tag value: entity encodings (walls/agents/items/pods/drop-offs/destinations 1, doors 0.6666 closed /
       // 0.4444 open, dirt = amount)
@@ -2996,7 +2988,8 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       };
       if constexpr (FLAT) {  // stash: the flattened pass below writes the layers (each lane only its own cell here)
         ctag[wi] = tags | ((m & CM_DCLOSED) ? CT_CLOSED : 0u);
-        ((tu64*)amw)[wi] = amask;
+        amw[2 * wi] = (uint32_t)amask;
+        amw[2 * wi + 1] = (uint32_t)(amask >> 32);
         if (wide) {
           const uint32_t w0v = amw2[2 * wi], w1v = amw2[2 * wi + 1];
           amw2[2 * wi] = v ? w0v : 0u;
@@ -3090,14 +3083,11 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
       tbl_sync<LR>();
       const int ne = nl * dd;
       const float invdd = 1.0f / (float)dd;
-#if MFG_OBS_SEL2
-      const double batv = frozen ? e.fbat()[a] : e.bat()[a];  // a Battery layer's one value (its first cell)
-#endif
       for (int e0 = 0; e0 < ne; e0 += MFG_WAVE) {
         const int el = min(e0 + lane, ne - 1);
         const int l = (int)(((float)el + 0.5f) * invdd), c = el - l * dd;
         const uint32_t ct = ctag[c];
-        const u64 am = ((const tu64*)amw)[c];  // one 64-bit read: lanes c and c + 16 on different banks
+        const u64 am = (u64)amw[2 * c] | ((u64)amw[2 * c + 1] << 32);
         const uint32_t tf = bperm(l, lr_tf);
         const uint64_t ab = (uint64_t)bperm(l, lr_alo) | ((uint64_t)bperm(l, lr_ahi) << 32);
         const uint32_t ut = tf & 0xFFFFu, fl = tf >> 16;
@@ -3107,19 +3097,7 @@ __device__ void build_obs(const Env& e, OT* out_env, int* pair_glob, const ObsPa
           cnt += popc(((u64)amw2[2 * c] | ((u64)amw2[2 * c + 1] << 32)) & ab2);
         }
         OT out = (OT)cnt;  // a small count: exact in OT
-#if MFG_OBS_SEL2
-        // doors and the battery, the special layers of most specs, by selects: the elements of one 64-value run span
-        // up to three layers, so a per-lane branch chain on the layer's flags diverged in most runs (C3: 4 of 6 per
-        // agent); the other special layers keep the branch below
-        {
-          const double dv = ((ct >> MFG_TAG_DOORS) & 1u) ? ((ct & CT_CLOSED) ? 0.6666 : 0.4444) : 0.0;
-          out = (fl & LR_DOOR) ? (OT)dv : out;
-          out = (fl & LR_BATTERY) ? (c == 0 ? (OT)batv : (OT)0) : out;
-        }
-        if (fl & ~(uint32_t)(LR_DOOR | LR_BATTERY)) {
-#else
         if (fl) {
-#endif
           auto tagv = [&](int tag) -> double {
             if (wide && tag >= MFG_TAG_AGENT0 + MFG_WAVE) {  // agents 64..127: the second mask table
               const int b = tag - MFG_TAG_AGENT0 - MFG_WAVE;
