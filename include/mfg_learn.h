@@ -27,6 +27,22 @@ int mfg_gru_bwd_step(const float* dout, int64_t do_row, const float* dhp_next, c
                      const float* hp_s, int64_t sv_row, float* dgi, int64_t dgi_row, float* dgh, int64_t dgh_row,
                      float* dhz, int64_t n, int hd, void* stream);
 
+/* the packed rows (idx u16 / val f32 [m, cap], a row's entries distinct, zero vals ignored) as dense f32 rows
+ * out [m][k] (row stride out_row >= k; k <= 4096): the learner's D for obs_proj's weight gradient D^T g (replaces a
+ * zero fill + scatter_add; marl.py _packed_grads). */
+int mfg_packed_densify(const uint16_t* idx, const float* val, int64_t m, int cap, int k, float* out, int64_t out_row,
+                       void* stream);
+
+/* out[r][:e_dim] = bias + sum_j val[r][j] wt[idx[r][j]] for the packed rows (wt [k][e_dim] = obs_proj.weight^T), the
+ * projection the render fuses (mfg_packed_obs.emb), for rows held outside a render (the learner's window slide). */
+int mfg_packed_project(const uint16_t* idx, const float* val, int64_t m, int cap, const float* wt, const float* bias,
+                       int e_dim, int k, float* out, int64_t out_row, void* stream);
+
+/* out[r] ~ Categorical(logits = logits[r][:n_act]) by inversion at u[r] in [0, 1) (the acting step's
+ * Categorical(logits).sample(), base_ac.py:74-76, with the uniforms drawn by the caller) */
+int mfg_sample_categorical(const float* logits, int64_t logit_row, int n_act, const float* u, int64_t n, int32_t* out,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

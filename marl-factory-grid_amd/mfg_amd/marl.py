@@ -157,18 +157,7 @@ class RecurrentAC(nn.Module):
         n, t = obs_emb.shape[:2]
         # learner windows with grad: the same layers with their weight gradients as split-K GEMMs (_tall_tn)
         sk = t > 1 and torch.is_grad_enabled()
-        action_emb = _Embed.apply(actions + 1, self.action_emb.weight, self.action_emb.padding_idx) if sk else \
-            self.action_emb(actions + 1)  # shift by one: padding idx (networks.py:53)
-        if not self.use_agent_embedding:
-            x_t = torch.cat((obs_emb, action_emb), -1)
-        else:
-            ids = agent_ids if agent_ids is not None else torch.arange(n, device=obs_emb.device)
-            agent_emb = self.agent_emb(ids.view(-1, 1).expand(n, t))
-            x_t = torch.cat((obs_emb, agent_emb, action_emb), -1)
-        if sk:
-            mixed = _lin(self.mix[3], torch.tanh(_lin(self.mix[1], torch.tanh(x_t))))
-        else:
-            mixed = self.mix(x_t)
+        mixed = self.mixed(obs_emb, actions, agent_ids, sk)
         ha = hidden_actor[:, 0]
         hc = hidden_critic[:, 0]
         if t == 1 and (starts is None or not bool(starts.any())):  # acting: one fused cell per GRU
@@ -201,6 +190,25 @@ class RecurrentAC(nn.Module):
                 ps.append(ha)
                 cs.append(hc)
             out_p, out_c = torch.stack(ps, 1), torch.stack(cs, 1)
+        return self._heads(out_p, out_c, sk)
+
+    def mixed(self, obs_emb, actions, agent_ids=None, sk=False):
+        """The GRUs' input: mix(cat(obs_emb, [agent_emb,] action_emb)) (networks.py:52-58); sk = the learner's
+        split-K weight gradients."""
+        n, t = obs_emb.shape[:2]
+        action_emb = _Embed.apply(actions + 1, self.action_emb.weight, self.action_emb.padding_idx) if sk else \
+            self.action_emb(actions + 1)  # shift by one: padding idx (networks.py:53)
+        if not self.use_agent_embedding:
+            x_t = torch.cat((obs_emb, action_emb), -1)
+        else:
+            ids = agent_ids if agent_ids is not None else torch.arange(n, device=obs_emb.device)
+            agent_emb = self.agent_emb(ids.view(-1, 1).expand(n, t))
+            x_t = torch.cat((obs_emb, agent_emb, action_emb), -1)
+        if sk:
+            return _lin(self.mix[3], torch.tanh(_lin(self.mix[1], torch.tanh(x_t))))
+        return self.mix(x_t)
+
+    def _heads(self, out_p, out_c, sk):
         if sk:
             logits = _lin(self.action_head[2], torch.tanh(_lin(self.action_head[0], out_p)))
             critic = _lin(self.critic_head[2], torch.tanh(_lin(self.critic_head[0], out_c))).squeeze(-1)
@@ -208,6 +216,19 @@ class RecurrentAC(nn.Module):
             logits = self.action_head(out_p)
             critic = self.critic_head(out_c).squeeze(-1)
         return dict(logits=logits, critic=critic, hidden_actor=out_p, hidden_critic=out_c)
+
+    def forward_saved(self, obs_emb, actions, agent_ids, starts, saved):
+        """forward_emb over a window whose recurrent pass already ran while acting with the same weights (the
+        GRU outputs and gate activations of every entry in `saved`, _GRUSaved): the input layers and heads are
+        evaluated with grad, the GRUs' forward is taken from `saved` and their backward runs on it."""
+        n, t = obs_emb.shape[:2]
+        mixed = self.mixed(obs_emb, actions, agent_ids, True)
+        keep = (~starts).to(mixed.dtype)
+        ga, gc = self.gru_actor, self.gru_critic
+        out_p, out_c = _GRUWindowSaved.apply(mixed, keep, saved, ga.weight_ih_l0, ga.weight_hh_l0, ga.bias_ih_l0,
+                                             ga.bias_hh_l0, gc.weight_ih_l0, gc.weight_hh_l0, gc.bias_ih_l0,
+                                             gc.bias_hh_l0)
+        return self._heads(out_p, out_c, True)
 
 
 class _Segments:
@@ -309,7 +330,82 @@ class _EngineProj(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         idx, val = ctx.saved_tensors
-        return None, None, _packed_weight_grad(idx, val, g, ctx.k).t(), g.sum(0), None
+        gw, gb = _packed_grads(idx, val, g, ctx.k)
+        return None, None, gw, gb, None
+
+
+def _packed_grads(idx, val, g, k):
+    """obs_proj's (weight [E, k], bias [E]) gradients from packed rows idx / val [M, cap] and g [M, E]: D^T g with D
+    the rows made dense (on the GPU by mfg_packed_densify, include/mfg_learn.h: one coalesced pass, no zero fill
+    or scatter_add), one split-K GEMM per block of <= 512 MiB of dense rows, and the column sums of g."""
+    if not (g.is_cuda and idx.dtype == torch.uint16):
+        return _packed_weight_grad(idx.long(), val, g, k).t(), g.sum(0)
+    L, st = _gru_lib(), torch.cuda.current_stream(g.device).cuda_stream
+    idx, val = idx.contiguous(), val.contiguous()
+    gw = None
+    step = max(1, (1 << 27) // max(k, 1))
+    for r0 in range(0, idx.shape[0], step):
+        rows = min(step, idx.shape[0] - r0)
+        d = torch.empty((rows, k), dtype=g.dtype, device=g.device)
+        if L.mfg_packed_densify(idx[r0].data_ptr(), val[r0].data_ptr(), rows, idx.shape[1], k, d.data_ptr(), k, st):
+            raise RuntimeError('mfg_packed_densify failed')
+        part = _tall_tn(g[r0:r0 + rows], d)  # [E, k]
+        gw = part if gw is None else gw + part
+    return gw, g.sum(0)
+
+
+def _project_dense(idx, val, proj):
+    """obs_proj over packed rows without grad: the rows scattered to dense blocks (<= 512 MiB) and one GEMM each
+    (embedding_bag with per-sample weights ran 0.77 ms for C3's 65,536 rows on the MI355X)."""
+    lead, cap = idx.shape[:-1], idx.shape[-1]
+    idx2, val2 = idx.reshape(-1, cap).long(), val.reshape(-1, cap)
+    k = proj.weight.shape[1]
+    out = torch.empty((idx2.shape[0], proj.weight.shape[0]), dtype=proj.weight.dtype, device=idx2.device)
+    step = max(1, (1 << 27) // max(k, 1))
+    for r0 in range(0, idx2.shape[0], step):
+        d = torch.zeros((min(step, idx2.shape[0] - r0), k), dtype=proj.weight.dtype, device=idx2.device)
+        d.scatter_add_(1, idx2[r0:r0 + step], val2[r0:r0 + step].to(d.dtype))
+        torch.addmm(proj.bias, d, proj.weight.t(), out=out[r0:r0 + step])
+    return out.view(*lead, -1)
+
+
+class _EngineProj(torch.autograd.Function):
+    """obs_proj(obs) for the learner, forward taken from the engine: every slot of the window was rendered with
+    the current weights (the fused projection of k_obs, MFG_OBS_PACKED), so the forward is that output (bias
+    included) and only the backward touches the packed rows (weight: D^T g, bias: the row sum of g)."""
+
+    @staticmethod
+    def forward(ctx, idx, val, weight, bias, emb):
+        ctx.save_for_backward(idx, val)
+        ctx.k = weight.shape[1]
+        return emb.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, val = ctx.saved_tensors
+        gw, gb = _packed_grads(idx, val, g, ctx.k)
+        return None, None, gw, gb, None
+
+
+def _packed_grads(idx, val, g, k):
+    """obs_proj's (weight [E, k], bias [E]) gradients from packed rows idx / val [M, cap] and g [M, E]: on the GPU
+    one HIP kernel pair (mfg_packed_wgrad, include/mfg_learn.h: per-CU LDS tiles, ~10x fewer products than the dense
+    GEMM and no dense rows); else the dense rows and one GEMM per block (_packed_weight_grad)."""
+    e_dim = g.shape[1]
+    if g.is_cuda and idx.dtype == torch.uint16 and g.dtype == torch.float32:
+        L = _gru_lib()
+        if L.mfg_packed_wgrad_ecw(e_dim, k) > 0:
+            idx, val, g = idx.contiguous(), val.contiguous(), g.contiguous()
+            part = torch.empty(_WGRAD_PARTS * (k + 1) * e_dim, dtype=g.dtype, device=g.device)
+            gw = torch.empty((e_dim, k), dtype=g.dtype, device=g.device)
+            gb = torch.empty((e_dim,), dtype=g.dtype, device=g.device)
+            rc = L.mfg_packed_wgrad(idx.data_ptr(), val.data_ptr(), idx.shape[0], idx.shape[1], g.data_ptr(), e_dim,
+                                    k, part.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                                    torch.cuda.current_stream(g.device).cuda_stream)
+            if rc:
+                raise RuntimeError('mfg_packed_wgrad failed')
+            return gw, gb
+    return _packed_weight_grad(idx.long(), val, g, k).t(), g.sum(0)
 
 
 _GRU_LIB = None
@@ -327,6 +423,12 @@ def _gru_lib():
         L.mfg_gru_fwd_step.restype = C.c_int
         L.mfg_gru_bwd_step.argtypes = [p, i64, p, p, i64, p, p, p, p, p, i64, p, i64, p, i64, p, i64, C.c_int, p]
         L.mfg_gru_bwd_step.restype = C.c_int
+        L.mfg_packed_densify.argtypes = [p, p, i64, C.c_int, C.c_int, p, i64, p]
+        L.mfg_packed_densify.restype = C.c_int
+        L.mfg_packed_project.argtypes = [p, p, i64, C.c_int, p, p, C.c_int, C.c_int, p, i64, p]
+        L.mfg_packed_project.restype = C.c_int
+        L.mfg_sample_categorical.argtypes = [p, i64, C.c_int, p, i64, p, p]
+        L.mfg_sample_categorical.restype = C.c_int
         _GRU_LIB = L
     return _GRU_LIB
 
@@ -409,12 +511,15 @@ class _GRUWindow(torch.autograd.Function):
         n, t, i_dim = x.shape
         dgis, grads = [], []
         gpu = _use_gru_kernels(x)
+        g_all = 3 * (ha_dim + hc_dim)
+        # GPU: both GRUs' input-gate gradients straight into one [n, t, 3Ha + 3Hc] buffer (no concatenation)
+        dgi_all = torch.empty((n, t, g_all), dtype=x.dtype, device=x.device) if gpu else None
         for gi_idx, (dout, wh, hd) in enumerate(((douta, wha, ha_dim), (doutc, whc, hc_dim))):
             hps, rs, zs, ns, ghns = saved[5 * gi_idx:5 * gi_idx + 5]
             if gpu:  # per step: one fused elementwise kernel (mfg_gru_bwd_step) + the recurrent GEMM
                 L, st = _gru_lib(), torch.cuda.current_stream(x.device).cuda_stream
-                dgi = torch.empty((n, t, 3 * hd), dtype=x.dtype, device=x.device)
-                dgh = torch.empty_like(dgi)
+                dgi = dgi_all[:, :, 3 * ha_dim * gi_idx:]
+                dgh = torch.empty((n, t, 3 * hd), dtype=x.dtype, device=x.device)
                 dout = None if dout is None else dout.contiguous()
                 sv_row = hps.stride(0)
                 dhp = None
@@ -424,12 +529,11 @@ class _GRUWindow(torch.autograd.Function):
                                             None if dhp is None else keep[:, s + 1].data_ptr(), t,
                                             rs[:, s].data_ptr(), zs[:, s].data_ptr(), ns[:, s].data_ptr(),
                                             ghns[:, s].data_ptr(), hps[:, s].data_ptr(), sv_row,
-                                            dgi[:, s].data_ptr(), t * 3 * hd, dgh[:, s].data_ptr(), t * 3 * hd,
+                                            dgi[:, s].data_ptr(), t * g_all, dgh[:, s].data_ptr(), t * 3 * hd,
                                             dhz.data_ptr(), n, hd, st)
                     if rc:
                         raise RuntimeError('mfg_gru_bwd_step failed')
                     dhp = torch.addmm(dhz, dgh[:, s], wh)
-                dgis.append(dgi)
                 dgh2 = dgh.reshape(n * t, 3 * hd)
                 grads.append((_tall_tn(dgh2, hps.reshape(n * t, hd)), dgh2.sum(0)))
                 continue
@@ -453,13 +557,32 @@ class _GRUWindow(torch.autograd.Function):
             dgis.append(dgi)
             dgh2 = dgh.reshape(n * t, 3 * hd)
             grads.append((_tall_tn(dgh2, hps.reshape(n * t, hd)), dgh2.sum(0)))  # dW_hh, db_hh
-        dgi_all = torch.cat(dgis, 2).reshape(n * t, -1)
+        dgi_all = (dgi_all if gpu else torch.cat(dgis, 2)).reshape(n * t, -1)
         dwi = _tall_tn(dgi_all, x.reshape(n * t, i_dim))  # [3Ha + 3Hc, I]
         dbi = dgi_all.sum(0)
         dx = (dgi_all @ wi).view(n, t, i_dim)
         sa = 3 * ha_dim
         return (dx, None, None, None, dwi[:sa], grads[0][0], dbi[:sa], grads[0][1],
                 dwi[sa:], grads[1][0], dbi[sa:], grads[1][1])
+
+
+class _GRUWindowSaved(torch.autograd.Function):
+    """_GRUWindow whose forward already ran: saved = (hs_a, hs_c, sv_a, sv_c), the outputs [N, T, H] and gate
+    activations (hp, r, z, n, gh_n, each [N, T, H]) the acting steps wrote with mfg_gru_fwd_step under the same
+    weights (BatchedA2C reuse_acting). The forward returns the stored outputs; the backward is _GRUWindow's."""
+
+    @staticmethod
+    def forward(ctx, x, keep, saved, wia, wha, bia, bha, wic, whc, bic, bhc):
+        hs_a, hs_c, sv_a, sv_c = saved
+        wi = torch.cat([wia, wic], 0)
+        ctx.save_for_backward(x, keep.contiguous(), wi, wha, whc, *sv_a, *sv_c)
+        ctx.dims = (wha.shape[1], whc.shape[1])
+        return hs_a.clone(), hs_c.clone()
+
+    @staticmethod
+    def backward(ctx, douta, doutc):
+        g = _GRUWindow.backward(ctx, douta, doutc)
+        return (g[0], None, None) + tuple(g[4:])
 
 
 def _gru_cell(gi, h, gru):
@@ -489,8 +612,12 @@ def compute_advantages(critic, reward, done, gamma, gae_coef=0.0):
 def a2c_loss(out, actions, reward, done, gamma, entropy_coef, vf_coef, gae_coef=0.0):
     """base_ac.py:200-217 on a forward output: actions [N, T+1] (entry 0 = the action before the window),
     reward / done [N, T] (the targets of entries 1..T)."""
-    logits = out['logits'][:, :-1]
-    critic = out['critic']
+    return a2c_loss_terms(out['logits'][:, :-1], out['critic'], actions, reward, done, gamma, entropy_coef, vf_coef,
+                          gae_coef)
+
+
+def a2c_loss_terms(logits, critic, actions, reward, done, gamma, entropy_coef, vf_coef, gae_coef=0.0):
+    """a2c_loss on the policy logits of entries 0..T-1 [N, T, n_act] and the critic of entries 0..T [N, T+1]."""
     entropy_loss = Categorical(logits=logits, validate_args=False).entropy().mean(-1)
     advantages = compute_advantages(critic, reward, done, gamma, gae_coef)
     value_loss = advantages.pow(2).mean(-1)
@@ -524,7 +651,7 @@ class BatchedA2C:
 
     def __init__(self, factory, net=None, n_steps=5, gamma=0.99, entropy_coef=0.01, vf_coef=0.5, gae_coef=0.0,
                  lr=3e-4, cap=32, obs_emb_size=96, action_emb_size=16, hidden_size=64, use_agent_embedding=False,
-                 check_cap=True, generator=None, engine_emb=True, graph=False, act_graph=False):
+                 check_cap=True, generator=None, engine_emb=True, graph=False, act_graph=False, reuse_acting=True):
         from .engine import PackedObs
         self.f = factory
         eng = factory.engine
@@ -572,6 +699,19 @@ class BatchedA2C:
         self.h0c = torch.zeros((N, 1, self.net.hidden_size_critic), device=dev)
         self.ha, self.hc = self.h0a.clone(), self.h0c.clone()  # persistent: updated in place (graph inputs)
         self._ha_new, self._hc_new = self.h0a.clone(), self.h0c.clone()  # the policy step's new states (static)
+        # reuse_acting: the acting steps run both GRUs through mfg_gru_fwd_step and keep every entry's outputs and
+        # gate activations (the weights are fixed over a window, so they ARE the learner's recurrent forward of
+        # entries 0..T-1); the learner then evaluates only the input layers, heads and loss with grad, the entry-T
+        # bootstrap critic without grad, and runs the GRU backward on the stored activations (no window recompute)
+        self.reuse = bool(reuse_acting) and self.dev.type == 'cuda'
+        if self.reuse:
+            Ha, Hc = H, self.net.hidden_size_critic
+            self.hs_a = torch.zeros((N, T, Ha), device=dev)
+            self.hs_c = torch.zeros((N, T, Hc), device=dev)
+            self.sv_a = torch.zeros((5, N, T, Ha), device=dev)  # hp, r, z, n, gh_n
+            self.sv_c = torch.zeros((5, N, T, Hc), device=dev)
+            self._one = torch.ones(1, device=dev)
+        self._u = torch.empty(N, device=dev)  # the sampling uniforms (static: graph-captured acting)
         self.last_loss = torch.zeros((), device=dev)
         self.agent_ids = torch.arange(self.A, device=dev).repeat(self.B)
         self.t = 0
@@ -602,26 +742,66 @@ class BatchedA2C:
         a = self.act[t].long()
         self.act_in[t + 1].copy_(torch.where(d.view(-1, 1), torch.full_like(a, -1), a))
         keep = (~d).to(self.ha.dtype).view(self.B, 1, 1)  # broadcast over the env's agents
-        torch.mul(self._ha_new.view(self.B, self.A, -1), keep, out=self.ha.view(self.B, self.A, -1))
-        torch.mul(self._hc_new.view(self.B, self.A, -1), keep, out=self.hc.view(self.B, self.A, -1))
+        ha_new, hc_new = (self.hs_a[:, t], self.hs_c[:, t]) if self.reuse else (self._ha_new, self._hc_new)
+        torch.mul(ha_new.view(self.B, self.A, -1), keep, out=self.ha.view(self.B, self.A, -1))
+        torch.mul(hc_new.view(self.B, self.A, -1), keep, out=self.hc.view(self.B, self.A, -1))
         self.t += 1
         if self.t == self.T:
             self.learn()
 
     def _policy(self, t):
         """Acting at window slot t: the policy on (o_t, a_{t-1}, h_t), an action per agent into act[t], the new
-        recurrent states into the static _ha_new / _hc_new."""
+        recurrent states into the static _ha_new / _hc_new (reuse_acting: into hs_a / hs_c [:, t], with the gate
+        activations into sv_a / sv_c [:, :, t]; the critic head is the learner's alone then)."""
         emb = self.pobs.emb[t].view(self.N, 1, -1)
         a_in = self.act_in[t].view(self.N, 1)
+        if self.reuse:
+            self._gru_step(self.net.mixed(emb, a_in, self.agent_ids)[:, 0], t)
+            self._sample(self.net.action_head(self.hs_a[:, t]), t)
+            return
         out = self.net.forward_emb(emb, a_in, self.ha, self.hc, agent_ids=self.agent_ids)
-        logits = out['logits'][:, 0]
-        if self.gen is None:
-            a = Categorical(logits=logits, validate_args=False).sample()
-        else:
-            a = torch.multinomial(torch.softmax(logits, -1), 1, generator=self.gen).squeeze(-1)
-        self.act[t].copy_(a.view(self.B, self.A))
+        self._sample(out['logits'][:, 0], t)
         self._ha_new.copy_(out['hidden_actor'])
         self._hc_new.copy_(out['hidden_critic'])
+
+    def _gru_step(self, x, t):
+        """Both GRU cells of entry t on x [N, I] (one input-gate GEMM for both, one recurrent GEMM and one
+        mfg_gru_fwd_step each), storing outputs and activations at entry t of the window buffers."""
+        net, N, T = self.net, self.N, self.T
+        ga, gc = net.gru_actor, net.gru_critic
+        gi = torch.addmm(torch.cat([ga.bias_ih_l0, gc.bias_ih_l0]), x, torch.cat([ga.weight_ih_l0, gc.weight_ih_l0]).t())
+        L, st = _gru_lib(), torch.cuda.current_stream(self.dev).cuda_stream
+        lo = 0
+        for (h, gru, hs, sv) in ((self.ha, ga, self.hs_a, self.sv_a), (self.hc, gc, self.hs_c, self.sv_c)):
+            hd = hs.shape[-1]
+            h2 = h[:, 0]
+            gh0 = h2 @ gru.weight_hh_l0.t()
+            rc = L.mfg_gru_fwd_step(gi[:, lo:].data_ptr(), gi.shape[1], gh0.data_ptr(), gru.bias_hh_l0.data_ptr(),
+                                    h2.data_ptr(), hd, self._one.data_ptr(), 0, hs[:, t].data_ptr(), T * hd,
+                                    sv[0, :, t].data_ptr(), sv[1, :, t].data_ptr(), sv[2, :, t].data_ptr(),
+                                    sv[3, :, t].data_ptr(), sv[4, :, t].data_ptr(), T * hd, N, hd, st)
+            if rc:
+                raise RuntimeError('mfg_gru_fwd_step failed')
+            lo += 3 * hd
+
+    def _sample(self, logits, t):
+        """a_t ~ Categorical(logits) per agent into act[t] (base_ac.py:74-76): on the GPU one kernel
+        (mfg_sample_categorical) on uniforms drawn into a static buffer; an explicit generator keeps
+        torch.multinomial."""
+        if self.gen is not None:
+            a = torch.multinomial(torch.softmax(logits, -1), 1, generator=self.gen).squeeze(-1)
+            self.act[t].copy_(a.view(self.B, self.A))
+            return
+        if not logits.is_cuda:
+            self.act[t].copy_(Categorical(logits=logits, validate_args=False).sample().view(self.B, self.A))
+            return
+        logits = logits.contiguous()
+        self._u.uniform_()
+        rc = _gru_lib().mfg_sample_categorical(logits.data_ptr(), logits.stride(0), logits.shape[1],
+                                               self._u.data_ptr(), self.N, self.act[t].data_ptr(),
+                                               torch.cuda.current_stream(self.dev).cuda_stream)
+        if rc:
+            raise RuntimeError('mfg_sample_categorical failed')
 
     def _policy_step(self, t):
         if not self.act_graph:
@@ -660,12 +840,48 @@ class BatchedA2C:
 
     def loss(self):
         """The A2C loss of the current window (base_ac.py:200-217), with grad."""
+        if self.reuse:
+            return self._loss_saved()
+        return self._loss_recompute()
+
+    def _loss_saved(self):
+        """loss() from the acting steps' stored recurrent pass (reuse_acting): entries 0..T-1 with grad through
+        the input layers, _GRUWindowSaved and the heads; the entry-T critic (the bootstrap target, detached in
+        base_ac.py:185-198) by one no-grad step from the carried state."""
+        T, N, cap = self.T, self.N, self.pobs.cap
+        net = self.net
+        idx = self.pobs.idx[:T].permute(1, 2, 0, 3).reshape(N * T, cap)
+        val = self.pobs.val[:T].permute(1, 2, 0, 3).reshape(N * T, cap)
+        a_in = self.act_in.permute(1, 2, 0).reshape(N, T + 1)
+        acts = torch.cat([a_in[:, :1], self.act.permute(1, 2, 0).reshape(N, T).long()], 1)
+        d = self.done.permute(1, 0).repeat_interleave(self.A, 0).to(torch.float32)  # [N, T]
+        starts = torch.cat([torch.zeros((N, 1), dtype=torch.bool, device=self.dev), d[:, :T - 1].bool()], 1)
+        rew = self.rew.permute(1, 2, 0).reshape(N, T).to(torch.float32)
+        with torch.no_grad():
+            xT = net.mixed(self.pobs.emb[T].view(N, 1, -1), self.act_in[T].view(N, 1), self.agent_ids)[:, 0]
+            gc = net.gru_critic
+            hT = torch.gru_cell(xT, self.hc[:, 0], gc.weight_ih_l0, gc.weight_hh_l0, gc.bias_ih_l0, gc.bias_hh_l0)
+            critic_T = net.critic_head(hT)  # [N, 1]
+        with torch.enable_grad():
+            if self.engine_emb:
+                emb_pre = self.pobs.emb[:T].permute(1, 2, 0, 3).reshape(N * T, -1)
+                emb = _EngineProj.apply(idx, val, net.obs_proj.weight, net.obs_proj.bias, emb_pre).view(N, T, -1)
+            else:
+                emb = net.project_packed(idx.view(N, T, cap), val.view(N, T, cap))
+            out = net.forward_saved(emb, a_in[:, :T], self.agent_ids, starts,
+                                    (self.hs_a, self.hs_c, list(self.sv_a.unbind(0)), list(self.sv_c.unbind(0))))
+            critic = torch.cat([out['critic'], critic_T], 1)
+            return a2c_loss_terms(out['logits'], critic, acts, rew, d, self.gamma, self.entropy_coef, self.vf_coef,
+                                  self.gae_coef)
+
+    def _loss_recompute(self):
+        """loss() with the whole window's forward recomputed (the reference learner's order, base_ac.py:126-128)."""
         idx, val, a_in, acts, starts, rew, d = self.window()
         with torch.enable_grad():
             if self.engine_emb:  # the forward from the render's fused projection (same weights), no gather
                 T, N, cap = self.T, self.N, idx.shape[-1]
                 emb_pre = self.pobs.emb.permute(1, 2, 0, 3).reshape(N * (T + 1), -1)
-                emb = _EngineProj.apply(idx.reshape(-1, cap).long(), val.reshape(-1, cap), self.net.obs_proj.weight,
+                emb = _EngineProj.apply(idx.reshape(-1, cap), val.reshape(-1, cap), self.net.obs_proj.weight,
                                         self.net.obs_proj.bias, emb_pre).view(N, T + 1, -1)
             else:
                 emb = self.net.project_packed(idx, val)
@@ -719,7 +935,20 @@ class BatchedA2C:
             self.h0c.copy_(self.hc)
             # new weights: the engine projects with them from now on; o_0's projection is redone here
             self.pobs.set_projection(self.net.obs_proj.weight, self.net.obs_proj.bias)
-            self.pobs.emb[0].copy_(_project_dense(self.pobs.idx[0], self.pobs.val[0], self.net.obs_proj))
+            self._project_slot0()
+
+    def _project_slot0(self):
+        """o_0's fused projection redone with the new weights (the engine rendered it with the old ones): one
+        mfg_packed_project over its packed rows on the GPU."""
+        pb = self.pobs
+        if not pb.idx.is_cuda:
+            pb.emb[0].copy_(_project_dense(pb.idx[0], pb.val[0], self.net.obs_proj))
+            return
+        rc = _gru_lib().mfg_packed_project(pb.idx[0].data_ptr(), pb.val[0].data_ptr(), self.N, pb.cap, pb.wt.data_ptr(),
+                                           pb.bias.data_ptr(), pb.E, pb.kdim, pb.emb[0].data_ptr(), pb.E,
+                                           torch.cuda.current_stream(self.dev).cuda_stream)
+        if rc:
+            raise RuntimeError('mfg_packed_project failed')
 
     def train(self, n_updates):
         for _ in range(n_updates * self.T):

@@ -244,9 +244,9 @@ def test_batched_a2c_act_graph_replays_the_policy():
     tr.train(4)
     assert sorted(tr._act_graphs) == list(range(5))
     tr._act_graphs[0].replay()
-    ha_g, hc_g = tr._ha_new.clone(), tr._hc_new.clone()
+    ha_g, hc_g, sv_g = tr.hs_a[:, 0].clone(), tr.hs_c[:, 0].clone(), tr.sv_a[:, :, 0].clone()
     tr._policy(0)
-    assert torch.equal(ha_g, tr._ha_new) and torch.equal(hc_g, tr._hc_new)
+    assert torch.equal(ha_g, tr.hs_a[:, 0]) and torch.equal(hc_g, tr.hs_c[:, 0]) and torch.equal(sv_g, tr.sv_a[:, :, 0])
     assert bool(torch.isfinite(tr.train(2)))
     assert int(tr.act.min()) >= 0 and int(tr.act.max()) < tr.n_actions
     f.close()
@@ -393,3 +393,115 @@ def test_gru_window_kernels_match_tensor_code(monkeypatch):
     for k in res[False][1]:
         a, b = res[True][1][k], res[False][1][k]
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), (k, (a - b).abs().max())
+
+
+@pytest.mark.gpu
+def test_batched_a2c_saved_window_matches_recompute():
+    """reuse_acting (the default): the learner takes the GRUs' forward from the acting steps (stored outputs and
+    gate activations) and evaluates the entry-T bootstrap critic by one no-grad step; loss and every gradient
+    equal the full-window recompute (the reference learner's order) within f32 tolerance."""
+    from mfg_amd.factory import BatchedFactory
+    from mfg_amd.marl import BatchedA2C
+    f = BatchedFactory('large8.yaml', 256, seed_base=4)
+    tr = BatchedA2C(f, n_steps=5, generator=torch.Generator(device='cuda').manual_seed(3))
+    assert tr.reuse
+    tr.train(2)  # weights moved away from init, episode restarts inside windows possible
+    learn, tr.learn = tr.learn, (lambda: None)
+    for _ in range(tr.T):
+        tr.step()
+    tr.learn = learn
+    res = {}
+    for name, fn in (('saved', tr._loss_saved), ('recompute', tr._loss_recompute)):
+        tr.net.zero_grad()
+        loss = fn()
+        loss.backward()
+        res[name] = (float(loss), {n: p.grad.detach().clone() for n, p in tr.net.named_parameters()
+                                   if p.grad is not None})
+    a, b = res['saved'][0], res['recompute'][0]
+    assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), (a, b)
+    assert set(res['saved'][1]) == set(res['recompute'][1])
+    for n, g in res['recompute'][1].items():
+        assert torch.allclose(res['saved'][1][n], g, rtol=1e-3, atol=1e-6), (n, (res['saved'][1][n] - g).abs().max())
+    f.close()
+
+
+def _rand_packed(m, cap, k, gen, fill=0.7):
+    """Random packed rows: distinct indices per row, nonzero values, ~fill of the cap slots used (zeros after)."""
+    idx = torch.zeros((m, cap), dtype=torch.int64)
+    val = torch.zeros((m, cap), dtype=torch.float32)
+    cnt = torch.randint(0, cap + 1, (m,), generator=gen)
+    cnt = torch.where(torch.rand(m, generator=gen) < fill, cnt, torch.full_like(cnt, cap))
+    perm = torch.rand((m, k), generator=gen).argsort(1)[:, :cap]
+    used = torch.arange(cap)[None, :] < cnt[:, None]
+    idx[used] = perm[used]
+    val[used] = torch.rand(int(used.sum()), generator=gen) * 2 + 0.25
+    return idx, val
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('m,cap,k,e', [(5000, 32, 343, 96), (3000, 70, 1000, 96), (777, 8, 50, 20)])
+def test_packed_grads_match_dense(m, cap, k, e):
+    """The learner's obs_proj gradients from packed rows (mfg_packed_densify, bit-exact dense rows, then the split-K
+    GEMM; C3's k = 343, a wide k = 1000, cap 70 past one wave) against the dense rows' f64 GEMM and column sum."""
+    import mfg_amd.marl as M
+    gen = torch.Generator().manual_seed(m)
+    idx, val = _rand_packed(m, cap, k, gen)
+    g = torch.randn((m, e), generator=gen)
+    d = torch.zeros((m, k), dtype=torch.float64)
+    d.scatter_add_(1, idx, val.double())
+    dd = torch.full((m, k + 3), -1.0, device='cuda')  # row stride k + 3: the pad columns stay untouched
+    iu, vc = idx.to(torch.uint16).cuda(), val.cuda()
+    assert M._gru_lib().mfg_packed_densify(iu.data_ptr(), vc.data_ptr(), m, cap, k, dd.data_ptr(), k + 3,
+                                           torch.cuda.current_stream().cuda_stream) == 0
+    assert torch.equal(dd[:, :k].cpu(), d.float()) and bool((dd[:, k:] == -1).all())
+    ref_w, ref_b = (d.t() @ g.double()).t(), g.double().sum(0)
+    gw, gb = M._packed_grads(iu, vc, g.cuda(), k)
+    assert gw.shape == (e, k) and gb.shape == (e,)
+    assert torch.allclose(gw.double().cpu(), ref_w, rtol=1e-4, atol=1e-4), (gw.double().cpu() - ref_w).abs().max()
+    assert torch.allclose(gb.double().cpu(), ref_b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_packed_project_kernel_matches_dense():
+    """mfg_packed_project (the learner's slot-0 re-projection) against bias + dense rows @ W^T in f64."""
+    import mfg_amd.marl as M
+    gen = torch.Generator().manual_seed(9)
+    m, cap, k, e = 4000, 70, 343, 96
+    idx, val = _rand_packed(m, cap, k, gen)
+    w, b = torch.randn((e, k), generator=gen), torch.randn(e, generator=gen)
+    d = torch.zeros((m, k), dtype=torch.float64)
+    d.scatter_add_(1, idx, val.double())
+    ref = d @ w.double().t() + b.double()
+    out = torch.empty((m, e), device='cuda')
+    L = M._gru_lib()
+    iu, vc, wt, bc = idx.to(torch.uint16).cuda(), val.cuda(), w.t().contiguous().cuda(), b.cuda()
+    assert L.mfg_packed_project(iu.data_ptr(), vc.data_ptr(), m, cap, wt.data_ptr(), bc.data_ptr(), e, k,
+                                out.data_ptr(), e, torch.cuda.current_stream().cuda_stream) == 0
+    assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_sample_categorical_kernel_distribution():
+    """mfg_sample_categorical: inversion sampling at caller-drawn uniforms; exact picks at chosen uniforms and the
+    empirical frequencies of 2M draws within 0.003 of softmax(logits)."""
+    import mfg_amd.marl as M
+    L = M._gru_lib()
+    st = torch.cuda.current_stream().cuda_stream
+    logits = torch.tensor([0.5, -1.0, 2.0, 0.0, 1.0], device='cuda')
+    p = torch.softmax(logits.double(), 0).cpu()
+    cdf = p.cumsum(0)
+    # exact picks: u just below / above each CDF step
+    us = torch.cat([cdf[:-1] - 1e-4, cdf[:-1] + 1e-4, torch.tensor([0.0, 0.999999])]).float().cuda()
+    n = us.numel()
+    lg = logits.repeat(n, 1).contiguous()
+    out = torch.empty(n, dtype=torch.int32, device='cuda')
+    assert L.mfg_sample_categorical(lg.data_ptr(), 5, 5, us.data_ptr(), n, out.data_ptr(), st) == 0
+    exp = torch.searchsorted(cdf, us.double().cpu(), right=True).clamp(max=4)
+    assert torch.equal(out.cpu().long(), exp)
+    n = 2_000_000
+    lg = logits.repeat(n, 1).contiguous()
+    u = torch.rand(n, device='cuda')
+    out = torch.empty(n, dtype=torch.int32, device='cuda')
+    assert L.mfg_sample_categorical(lg.data_ptr(), 5, 5, u.data_ptr(), n, out.data_ptr(), st) == 0
+    freq = torch.bincount(out.long(), minlength=5).double().cpu() / n
+    assert float((freq - p).abs().max()) < 3e-3, (freq, p)
