@@ -354,60 +354,6 @@ def _packed_grads(idx, val, g, k):
     return gw, g.sum(0)
 
 
-def _project_dense(idx, val, proj):
-    """obs_proj over packed rows without grad: the rows scattered to dense blocks (<= 512 MiB) and one GEMM each
-    (embedding_bag with per-sample weights ran 0.77 ms for C3's 65,536 rows on the MI355X)."""
-    lead, cap = idx.shape[:-1], idx.shape[-1]
-    idx2, val2 = idx.reshape(-1, cap).long(), val.reshape(-1, cap)
-    k = proj.weight.shape[1]
-    out = torch.empty((idx2.shape[0], proj.weight.shape[0]), dtype=proj.weight.dtype, device=idx2.device)
-    step = max(1, (1 << 27) // max(k, 1))
-    for r0 in range(0, idx2.shape[0], step):
-        d = torch.zeros((min(step, idx2.shape[0] - r0), k), dtype=proj.weight.dtype, device=idx2.device)
-        d.scatter_add_(1, idx2[r0:r0 + step], val2[r0:r0 + step].to(d.dtype))
-        torch.addmm(proj.bias, d, proj.weight.t(), out=out[r0:r0 + step])
-    return out.view(*lead, -1)
-
-
-class _EngineProj(torch.autograd.Function):
-    """obs_proj(obs) for the learner, forward taken from the engine: every slot of the window was rendered with
-    the current weights (the fused projection of k_obs, MFG_OBS_PACKED), so the forward is that output (bias
-    included) and only the backward touches the packed rows (weight: D^T g, bias: the row sum of g)."""
-
-    @staticmethod
-    def forward(ctx, idx, val, weight, bias, emb):
-        ctx.save_for_backward(idx, val)
-        ctx.k = weight.shape[1]
-        return emb.clone()
-
-    @staticmethod
-    def backward(ctx, g):
-        idx, val = ctx.saved_tensors
-        gw, gb = _packed_grads(idx, val, g, ctx.k)
-        return None, None, gw, gb, None
-
-
-def _packed_grads(idx, val, g, k):
-    """obs_proj's (weight [E, k], bias [E]) gradients from packed rows idx / val [M, cap] and g [M, E]: on the GPU
-    one HIP kernel pair (mfg_packed_wgrad, include/mfg_learn.h: per-CU LDS tiles, ~10x fewer products than the dense
-    GEMM and no dense rows); else the dense rows and one GEMM per block (_packed_weight_grad)."""
-    e_dim = g.shape[1]
-    if g.is_cuda and idx.dtype == torch.uint16 and g.dtype == torch.float32:
-        L = _gru_lib()
-        if L.mfg_packed_wgrad_ecw(e_dim, k) > 0:
-            idx, val, g = idx.contiguous(), val.contiguous(), g.contiguous()
-            part = torch.empty(_WGRAD_PARTS * (k + 1) * e_dim, dtype=g.dtype, device=g.device)
-            gw = torch.empty((e_dim, k), dtype=g.dtype, device=g.device)
-            gb = torch.empty((e_dim,), dtype=g.dtype, device=g.device)
-            rc = L.mfg_packed_wgrad(idx.data_ptr(), val.data_ptr(), idx.shape[0], idx.shape[1], g.data_ptr(), e_dim,
-                                    k, part.data_ptr(), gw.data_ptr(), gb.data_ptr(),
-                                    torch.cuda.current_stream(g.device).cuda_stream)
-            if rc:
-                raise RuntimeError('mfg_packed_wgrad failed')
-            return gw, gb
-    return _packed_weight_grad(idx.long(), val, g, k).t(), g.sum(0)
-
-
 _GRU_LIB = None
 
 
