@@ -33,6 +33,7 @@ from torch.distributions import Categorical
 
 
 SPLIT_ROWS = 2048  # rows per split of a tall-K weight-gradient GEMM (_tall_tn)
+TALL_SUM = 'sum'  # how _tall_tn sums its splits on the GPU: 'sum' (torch reduction) or 'gemv' (a ones-row GEMM)
 
 
 def _tall_tn(a, b, rows=None):
@@ -46,7 +47,11 @@ def _tall_tn(a, b, rows=None):
     if s < 2:
         return a.t() @ b
     k0 = s * rows
-    out = torch.bmm(a[:k0].reshape(s, rows, -1).transpose(1, 2), b[:k0].reshape(s, rows, -1)).sum(0)
+    parts = torch.bmm(a[:k0].reshape(s, rows, -1).transpose(1, 2), b[:k0].reshape(s, rows, -1))
+    if TALL_SUM == 'gemv' and parts.is_cuda:  # the split sum as one [1, s] x [s, m*n] product (a streaming read)
+        out = (torch.ones((1, s), dtype=parts.dtype, device=parts.device) @ parts.view(s, -1)).view(parts.shape[1:])
+    else:
+        out = parts.sum(0)
     if k0 < k:
         out = out + a[k0:].t() @ b[k0:]
     return out
@@ -216,19 +221,6 @@ class RecurrentAC(nn.Module):
             logits = self.action_head(out_p)
             critic = self.critic_head(out_c).squeeze(-1)
         return dict(logits=logits, critic=critic, hidden_actor=out_p, hidden_critic=out_c)
-
-    def forward_saved(self, obs_emb, actions, agent_ids, starts, saved):
-        """forward_emb over a window whose recurrent pass already ran while acting with the same weights (the
-        GRU outputs and gate activations of every entry in `saved`, _GRUSaved): the input layers and heads are
-        evaluated with grad, the GRUs' forward is taken from `saved` and their backward runs on it."""
-        n, t = obs_emb.shape[:2]
-        mixed = self.mixed(obs_emb, actions, agent_ids, True)
-        keep = (~starts).to(mixed.dtype)
-        ga, gc = self.gru_actor, self.gru_critic
-        out_p, out_c = _GRUWindowSaved.apply(mixed, keep, saved, ga.weight_ih_l0, ga.weight_hh_l0, ga.bias_ih_l0,
-                                             ga.bias_hh_l0, gc.weight_ih_l0, gc.weight_hh_l0, gc.bias_ih_l0,
-                                             gc.bias_hh_l0)
-        return self._heads(out_p, out_c, True)
 
 
 class _Segments:
@@ -512,23 +504,84 @@ class _GRUWindow(torch.autograd.Function):
                 dwi[sa:], grads[1][0], dbi[sa:], grads[1][1])
 
 
-class _GRUWindowSaved(torch.autograd.Function):
-    """_GRUWindow whose forward already ran: saved = (hs_a, hs_c, sv_a, sv_c), the outputs [N, T, H] and gate
-    activations (hp, r, z, n, gh_n, each [N, T, H]) the acting steps wrote with mfg_gru_fwd_step under the same
-    weights (BatchedA2C reuse_acting). The forward returns the stored outputs; the backward is _GRUWindow's."""
+class _MixSaved(torch.autograd.Function):
+    """RecurrentAC.mix (Tanh, Linear, Tanh, Linear; networks.py:24-25) over a window whose forward the acting steps
+    already ran with the same weights: saved = (ax, h1, mixed, a_prev, pad), ax = tanh(cat(obs_emb, action_emb))
+    [M, E + AE], h1 = tanh(ax W1^T + b1) [M, H], mixed [M, H] and the action inputs a_prev [M] (-1 = none). The
+    forward returns the stored output; the backward is the layers' chain rule (weight gradients by _tall_tn), with
+    the obs_emb gradient for obs_proj and the action-embedding gradient as onehot(a_prev + 1)^T g (padding row 0)."""
+
+    @staticmethod
+    def forward(ctx, emb, w1, b1, w3, b3, aw, saved):
+        ax, h1, mx, a_prev, pad = saved
+        ctx.save_for_backward(w1, w3, ax, h1, a_prev)
+        ctx.e_dim, ctx.n_emb, ctx.pad = emb.shape[1], aw.shape[0], pad
+        return mx.view_as(mx)
+
+    @staticmethod
+    def backward(ctx, g3):
+        w1, w3, ax, h1, a_prev = ctx.saved_tensors
+        g3 = g3.contiguous()
+        dw3, db3 = _tall_tn(g3, h1), g3.sum(0)
+        dz1 = (g3 @ w3) * (1.0 - h1 * h1)
+        dw1, db1 = _tall_tn(dz1, ax), dz1.sum(0)
+        dx = (dz1 @ w1) * (1.0 - ax * ax)
+        e = ctx.e_dim
+        oh = F.one_hot(a_prev + 1, ctx.n_emb).to(dx.dtype)
+        daw = _tall_tn(oh, dx[:, e:].contiguous())
+        if ctx.pad is not None:
+            daw[ctx.pad] = 0
+        return dx[:, :e], dw1, db1, dw3, db3, daw, None
+
+
+class _GRUWindowSavedT(torch.autograd.Function):
+    """Both GRUs over a window whose forward the acting steps already ran (mfg_gru_fwd_step) with the same weights,
+    entry-major: saved = (hs_a, hs_c, sv_a, sv_c), outputs [T, N, H] and gate activations [5, T, N, H] (hp, r, z, n,
+    gh_n); x [T*N, I] the GRUs' input, keep [T, N] (0 = an episode restart at that entry). The forward returns the
+    stored outputs; the backward is _GRUWindow's (per step one mfg_gru_bwd_step and the recurrent GEMM, then one GEMM
+    each for the input-weight, input and recurrent-weight gradients over all T*N rows) on entry-major rows."""
 
     @staticmethod
     def forward(ctx, x, keep, saved, wia, wha, bia, bha, wic, whc, bic, bhc):
         hs_a, hs_c, sv_a, sv_c = saved
         wi = torch.cat([wia, wic], 0)
-        ctx.save_for_backward(x, keep.contiguous(), wi, wha, whc, *sv_a, *sv_c)
-        ctx.dims = (wha.shape[1], whc.shape[1])
-        return hs_a.clone(), hs_c.clone()
+        ctx.save_for_backward(x, keep, wi, wha, whc, *sv_a.unbind(0), *sv_c.unbind(0))
+        t, n = keep.shape
+        return hs_a.view(t * n, -1), hs_c.view(t * n, -1)
 
     @staticmethod
     def backward(ctx, douta, doutc):
-        g = _GRUWindow.backward(ctx, douta, doutc)
-        return (g[0], None, None) + tuple(g[4:])
+        x, keep, wi, wha, whc, *sv = ctx.saved_tensors
+        t, n = keep.shape
+        ha_dim, hc_dim = wha.shape[1], whc.shape[1]
+        g_all = 3 * (ha_dim + hc_dim)
+        L, st = _gru_lib(), torch.cuda.current_stream(x.device).cuda_stream
+        dgi_all = torch.empty((t, n, g_all), dtype=x.dtype, device=x.device)
+        grads = []
+        for gidx, (dout, wh, hd) in enumerate(((douta, wha, ha_dim), (doutc, whc, hc_dim))):
+            hps, rs, zs, ns, ghns = sv[5 * gidx:5 * gidx + 5]
+            dgh = torch.empty((t, n, 3 * hd), dtype=x.dtype, device=x.device)
+            dout = None if dout is None else dout.contiguous().view(t, n, hd)
+            lo = 3 * ha_dim * gidx
+            dhp = None
+            for s in range(t - 1, -1, -1):
+                dhz = torch.empty((n, hd), dtype=x.dtype, device=x.device)
+                rc = L.mfg_gru_bwd_step(None if dout is None else dout[s].data_ptr(), hd, _ptr(dhp),
+                                        None if dhp is None else keep[s + 1].data_ptr(), 1,
+                                        rs[s].data_ptr(), zs[s].data_ptr(), ns[s].data_ptr(), ghns[s].data_ptr(),
+                                        hps[s].data_ptr(), hd, dgi_all[s, :, lo:].data_ptr(), g_all,
+                                        dgh[s].data_ptr(), 3 * hd, dhz.data_ptr(), n, hd, st)
+                if rc:
+                    raise RuntimeError('mfg_gru_bwd_step failed')
+                dhp = torch.addmm(dhz, dgh[s], wh)
+            dgh2 = dgh.view(t * n, 3 * hd)
+            grads.append((_tall_tn(dgh2, hps.reshape(t * n, hd)), dgh2.sum(0)))
+        dgi2 = dgi_all.view(t * n, g_all)
+        dwi, dbi = _tall_tn(dgi2, x), dgi2.sum(0)
+        dx = dgi2 @ wi
+        sa = 3 * ha_dim
+        return (dx, None, None, dwi[:sa], grads[0][0], dbi[:sa], grads[0][1], dwi[sa:], grads[1][0], dbi[sa:],
+                grads[1][1])
 
 
 def _gru_cell(gi, h, gru):
@@ -649,13 +702,20 @@ class BatchedA2C:
         # gate activations (the weights are fixed over a window, so they ARE the learner's recurrent forward of
         # entries 0..T-1); the learner then evaluates only the input layers, heads and loss with grad, the entry-T
         # bootstrap critic without grad, and runs the GRU backward on the stored activations (no window recompute)
-        self.reuse = bool(reuse_acting) and self.dev.type == 'cuda'
+        # (entry-major [T, N, ...] window buffers: an acting step writes one contiguous slice, and the learner's rows
+        # are the engine's slot order, so the packed rows and fused projection of the window are used in place)
+        self.reuse = bool(reuse_acting) and self.dev.type == 'cuda' and not self.net.use_agent_embedding
         if self.reuse:
             Ha, Hc = H, self.net.hidden_size_critic
-            self.hs_a = torch.zeros((N, T, Ha), device=dev)
-            self.hs_c = torch.zeros((N, T, Hc), device=dev)
-            self.sv_a = torch.zeros((5, N, T, Ha), device=dev)  # hp, r, z, n, gh_n
-            self.sv_c = torch.zeros((5, N, T, Hc), device=dev)
+            E, AE = self.net.obs_proj.weight.shape[0], self.net.action_emb_size
+            Hm = self.net.mix[1].weight.shape[0]
+            self.ax = torch.zeros((T, N, E + AE), device=dev)  # tanh(cat(obs_emb, action_emb)), the mix input
+            self.h1 = torch.zeros((T, N, Hm), device=dev)  # the mix's hidden tanh
+            self.mx = torch.zeros((T, N, self.net.mix[3].weight.shape[0]), device=dev)  # the GRUs' input
+            self.hs_a = torch.zeros((T, N, Ha), device=dev)
+            self.hs_c = torch.zeros((T, N, Hc), device=dev)
+            self.sv_a = torch.zeros((5, T, N, Ha), device=dev)  # hp, r, z, n, gh_n
+            self.sv_c = torch.zeros((5, T, N, Hc), device=dev)
             self._one = torch.ones(1, device=dev)
         self._u = torch.empty(N, device=dev)  # the sampling uniforms (static: graph-captured acting)
         self.last_loss = torch.zeros((), device=dev)
@@ -688,7 +748,7 @@ class BatchedA2C:
         a = self.act[t].long()
         self.act_in[t + 1].copy_(torch.where(d.view(-1, 1), torch.full_like(a, -1), a))
         keep = (~d).to(self.ha.dtype).view(self.B, 1, 1)  # broadcast over the env's agents
-        ha_new, hc_new = (self.hs_a[:, t], self.hs_c[:, t]) if self.reuse else (self._ha_new, self._hc_new)
+        ha_new, hc_new = (self.hs_a[t], self.hs_c[t]) if self.reuse else (self._ha_new, self._hc_new)
         torch.mul(ha_new.view(self.B, self.A, -1), keep, out=self.ha.view(self.B, self.A, -1))
         torch.mul(hc_new.view(self.B, self.A, -1), keep, out=self.hc.view(self.B, self.A, -1))
         self.t += 1
@@ -697,13 +757,21 @@ class BatchedA2C:
 
     def _policy(self, t):
         """Acting at window slot t: the policy on (o_t, a_{t-1}, h_t), an action per agent into act[t], the new
-        recurrent states into the static _ha_new / _hc_new (reuse_acting: into hs_a / hs_c [:, t], with the gate
-        activations into sv_a / sv_c [:, :, t]; the critic head is the learner's alone then)."""
+        recurrent states into the static _ha_new / _hc_new (reuse_acting: the mix activations into ax / h1 / mx [t],
+        the recurrent states into hs_a / hs_c [t] and the gate activations into sv_a / sv_c [:, t]; the critic head
+        is the learner's alone then)."""
         emb = self.pobs.emb[t].view(self.N, 1, -1)
         a_in = self.act_in[t].view(self.N, 1)
         if self.reuse:
-            self._gru_step(self.net.mixed(emb, a_in, self.agent_ids)[:, 0], t)
-            self._sample(self.net.action_head(self.hs_a[:, t]), t)
+            net, e = self.net, emb.shape[-1]
+            ax, h1, mx = self.ax[t], self.h1[t], self.mx[t]
+            # tanh(cat(obs_emb, action_emb)) as two writes into the slot (tanh is elementwise); then the two layers
+            torch.tanh(emb[:, 0], out=ax[:, :e])
+            ax[:, e:].copy_(torch.tanh(net.action_emb.weight)[self.act_in[t].view(-1) + 1])
+            torch.tanh(torch.addmm(net.mix[1].bias, ax, net.mix[1].weight.t()), out=h1)
+            torch.addmm(net.mix[3].bias, h1, net.mix[3].weight.t(), out=mx)
+            self._gru_step(mx, t)
+            self._sample(net.action_head(self.hs_a[t]), t)
             return
         out = self.net.forward_emb(emb, a_in, self.ha, self.hc, agent_ids=self.agent_ids)
         self._sample(out['logits'][:, 0], t)
@@ -723,9 +791,9 @@ class BatchedA2C:
             h2 = h[:, 0]
             gh0 = h2 @ gru.weight_hh_l0.t()
             rc = L.mfg_gru_fwd_step(gi[:, lo:].data_ptr(), gi.shape[1], gh0.data_ptr(), gru.bias_hh_l0.data_ptr(),
-                                    h2.data_ptr(), hd, self._one.data_ptr(), 0, hs[:, t].data_ptr(), T * hd,
-                                    sv[0, :, t].data_ptr(), sv[1, :, t].data_ptr(), sv[2, :, t].data_ptr(),
-                                    sv[3, :, t].data_ptr(), sv[4, :, t].data_ptr(), T * hd, N, hd, st)
+                                    h2.data_ptr(), hd, self._one.data_ptr(), 0, hs[t].data_ptr(), hd,
+                                    sv[0, t].data_ptr(), sv[1, t].data_ptr(), sv[2, t].data_ptr(), sv[3, t].data_ptr(),
+                                    sv[4, t].data_ptr(), hd, N, hd, st)
             if rc:
                 raise RuntimeError('mfg_gru_fwd_step failed')
             lo += 3 * hd
@@ -791,33 +859,42 @@ class BatchedA2C:
         return self._loss_recompute()
 
     def _loss_saved(self):
-        """loss() from the acting steps' stored recurrent pass (reuse_acting): entries 0..T-1 with grad through
-        the input layers, _GRUWindowSaved and the heads; the entry-T critic (the bootstrap target, detached in
-        base_ac.py:185-198) by one no-grad step from the carried state."""
-        T, N, cap = self.T, self.N, self.pobs.cap
+        """loss() from the acting steps' stored forward (reuse_acting), entry-major rows (t, n): obs_proj through
+        _EngineProj on the window's packed rows in place, the mix through _MixSaved and the GRUs through
+        _GRUWindowSavedT (stored forwards, backward only), the heads with grad; the entry-T critic (the bootstrap
+        target, detached in base_ac.py:185-198) by one no-grad step from the carried state."""
+        T, N, cap, A = self.T, self.N, self.pobs.cap, self.A
         net = self.net
-        idx = self.pobs.idx[:T].permute(1, 2, 0, 3).reshape(N * T, cap)
-        val = self.pobs.val[:T].permute(1, 2, 0, 3).reshape(N * T, cap)
-        a_in = self.act_in.permute(1, 2, 0).reshape(N, T + 1)
-        acts = torch.cat([a_in[:, :1], self.act.permute(1, 2, 0).reshape(N, T).long()], 1)
-        d = self.done.permute(1, 0).repeat_interleave(self.A, 0).to(torch.float32)  # [N, T]
-        starts = torch.cat([torch.zeros((N, 1), dtype=torch.bool, device=self.dev), d[:, :T - 1].bool()], 1)
-        rew = self.rew.permute(1, 2, 0).reshape(N, T).to(torch.float32)
+        rows = T * N
+        d = self.done.to(torch.float32).repeat_interleave(A, 1)  # [T, N]: done after entry t
+        keep = torch.ones((T, N), dtype=torch.float32, device=self.dev)
+        keep[1:] = 1.0 - d[:-1]  # entry s > 0 restarts after an episode end at s - 1
         with torch.no_grad():
             xT = net.mixed(self.pobs.emb[T].view(N, 1, -1), self.act_in[T].view(N, 1), self.agent_ids)[:, 0]
             gc = net.gru_critic
             hT = torch.gru_cell(xT, self.hc[:, 0], gc.weight_ih_l0, gc.weight_hh_l0, gc.bias_ih_l0, gc.bias_hh_l0)
             critic_T = net.critic_head(hT)  # [N, 1]
         with torch.enable_grad():
+            idx, val = self.pobs.idx[:T].reshape(rows, cap), self.pobs.val[:T].reshape(rows, cap)
             if self.engine_emb:
-                emb_pre = self.pobs.emb[:T].permute(1, 2, 0, 3).reshape(N * T, -1)
-                emb = _EngineProj.apply(idx, val, net.obs_proj.weight, net.obs_proj.bias, emb_pre).view(N, T, -1)
+                emb = _EngineProj.apply(idx, val, net.obs_proj.weight, net.obs_proj.bias,
+                                        self.pobs.emb[:T].reshape(rows, -1))
             else:
-                emb = net.project_packed(idx.view(N, T, cap), val.view(N, T, cap))
-            out = net.forward_saved(emb, a_in[:, :T], self.agent_ids, starts,
-                                    (self.hs_a, self.hs_c, list(self.sv_a.unbind(0)), list(self.sv_c.unbind(0))))
-            critic = torch.cat([out['critic'], critic_T], 1)
-            return a2c_loss_terms(out['logits'], critic, acts, rew, d, self.gamma, self.entropy_coef, self.vf_coef,
+                emb = net.project_packed(idx, val)
+            mixed = _MixSaved.apply(emb, net.mix[1].weight, net.mix[1].bias, net.mix[3].weight, net.mix[3].bias,
+                                    net.action_emb.weight, (self.ax.view(rows, -1), self.h1.view(rows, -1),
+                                                            self.mx.view(rows, -1), self.act_in[:T].reshape(rows),
+                                                            net.action_emb.padding_idx))
+            ga, gc = net.gru_actor, net.gru_critic
+            out_p, out_c = _GRUWindowSavedT.apply(mixed, keep, (self.hs_a, self.hs_c, self.sv_a, self.sv_c),
+                                                  ga.weight_ih_l0, ga.weight_hh_l0, ga.bias_ih_l0, ga.bias_hh_l0,
+                                                  gc.weight_ih_l0, gc.weight_hh_l0, gc.bias_ih_l0, gc.bias_hh_l0)
+            out = net._heads(out_p, out_c, True)
+            logits = out['logits'].view(T, N, -1).transpose(0, 1)  # [N, T, n_act]
+            critic = torch.cat([out['critic'].view(T, N).t(), critic_T], 1)  # [N, T + 1]
+            acts = torch.cat([self.act_in[0].reshape(N, 1), self.act.reshape(T, N).t().long()], 1)
+            rew = self.rew.reshape(T, N).t().to(torch.float32)
+            return a2c_loss_terms(logits, critic, acts, rew, d.t(), self.gamma, self.entropy_coef, self.vf_coef,
                                   self.gae_coef)
 
     def _loss_recompute(self):

@@ -244,9 +244,10 @@ def test_batched_a2c_act_graph_replays_the_policy():
     tr.train(4)
     assert sorted(tr._act_graphs) == list(range(5))
     tr._act_graphs[0].replay()
-    ha_g, hc_g, sv_g = tr.hs_a[:, 0].clone(), tr.hs_c[:, 0].clone(), tr.sv_a[:, :, 0].clone()
+    ha_g, hc_g, sv_g, mx_g = tr.hs_a[0].clone(), tr.hs_c[0].clone(), tr.sv_a[:, 0].clone(), tr.mx[0].clone()
     tr._policy(0)
-    assert torch.equal(ha_g, tr.hs_a[:, 0]) and torch.equal(hc_g, tr.hs_c[:, 0]) and torch.equal(sv_g, tr.sv_a[:, :, 0])
+    assert torch.equal(ha_g, tr.hs_a[0]) and torch.equal(hc_g, tr.hs_c[0]) and torch.equal(sv_g, tr.sv_a[:, 0])
+    assert torch.equal(mx_g, tr.mx[0])
     assert bool(torch.isfinite(tr.train(2)))
     assert int(tr.act.min()) >= 0 and int(tr.act.max()) < tr.n_actions
     f.close()
@@ -397,9 +398,9 @@ def test_gru_window_kernels_match_tensor_code(monkeypatch):
 
 @pytest.mark.gpu
 def test_batched_a2c_saved_window_matches_recompute():
-    """reuse_acting (the default): the learner takes the GRUs' forward from the acting steps (stored outputs and
-    gate activations) and evaluates the entry-T bootstrap critic by one no-grad step; loss and every gradient
-    equal the full-window recompute (the reference learner's order) within f32 tolerance."""
+    """reuse_acting (the default): the learner takes the mix's and the GRUs' forward from the acting steps (stored
+    activations, entry-major) and evaluates the entry-T bootstrap critic by one no-grad step; loss and every
+    gradient equal the full-window recompute (the reference learner's order) within f32 tolerance."""
     from mfg_amd.factory import BatchedFactory
     from mfg_amd.marl import BatchedA2C
     f = BatchedFactory('large8.yaml', 256, seed_base=4)
@@ -505,3 +506,28 @@ def test_sample_categorical_kernel_distribution():
     assert L.mfg_sample_categorical(lg.data_ptr(), 5, 5, u.data_ptr(), n, out.data_ptr(), st) == 0
     freq = torch.bincount(out.long(), minlength=5).double().cpu() / n
     assert float((freq - p).abs().max()) < 3e-3, (freq, p)
+
+
+def test_saved_mix_backward_matches_autograd():
+    """_MixSaved (the learner's mix from the acting steps' stored activations): forward == net.mix on the same
+    inputs and every gradient (obs_emb, both layers, the action embedding with its padding row) == autograd's."""
+    import mfg_amd.marl as M
+    torch.manual_seed(0)
+    net = M.RecurrentAC(40, 5, 24, 8, 16, 16, 4, use_agent_embedding=False)
+    rows = 300
+    emb = torch.randn(rows, 24, requires_grad=True)
+    a = torch.randint(-1, 5, (rows,))
+    params = [emb, net.mix[1].weight, net.mix[1].bias, net.mix[3].weight, net.mix[3].bias, net.action_emb.weight]
+    x = torch.cat([emb, net.action_emb(a + 1)], 1)
+    ref = net.mix(x)
+    g = torch.randn_like(ref)
+    gr = torch.autograd.grad(ref, params, g)
+    with torch.no_grad():
+        ax = torch.tanh(x)
+        h1 = torch.tanh(net.mix[1](ax))
+        mx = net.mix[3](h1)
+    out = M._MixSaved.apply(emb, *params[1:], (ax, h1, mx, a, net.action_emb.padding_idx))
+    gs = torch.autograd.grad(out, params, g)
+    assert torch.allclose(out, ref, atol=1e-6)
+    for p, q in zip(gs, gr):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6), (p - q).abs().max()
