@@ -33,7 +33,6 @@ from torch.distributions import Categorical
 
 
 SPLIT_ROWS = 2048  # rows per split of a tall-K weight-gradient GEMM (_tall_tn)
-TALL_SUM = 'sum'  # how _tall_tn sums its splits on the GPU: 'sum' (torch reduction) or 'gemv' (a ones-row GEMM)
 
 
 def _tall_tn(a, b, rows=None):
@@ -47,11 +46,8 @@ def _tall_tn(a, b, rows=None):
     if s < 2:
         return a.t() @ b
     k0 = s * rows
-    parts = torch.bmm(a[:k0].reshape(s, rows, -1).transpose(1, 2), b[:k0].reshape(s, rows, -1))
-    if TALL_SUM == 'gemv' and parts.is_cuda:  # the split sum as one [1, s] x [s, m*n] product (a streaming read)
-        out = (torch.ones((1, s), dtype=parts.dtype, device=parts.device) @ parts.view(s, -1)).view(parts.shape[1:])
-    else:
-        out = parts.sum(0)
+    # (the split sum as a ones-row GEMM instead measured slower: 4.60M vs 4.83M env-steps/s in the A2C loop)
+    out = torch.bmm(a[:k0].reshape(s, rows, -1).transpose(1, 2), b[:k0].reshape(s, rows, -1)).sum(0)
     if k0 < k:
         out = out + a[k0:].t() @ b[k0:]
     return out
@@ -523,9 +519,9 @@ class _MixSaved(torch.autograd.Function):
         w1, w3, ax, h1, a_prev = ctx.saved_tensors
         g3 = g3.contiguous()
         dw3, db3 = _tall_tn(g3, h1), g3.sum(0)
-        dz1 = (g3 @ w3) * (1.0 - h1 * h1)
+        dz1 = torch.ops.aten.tanh_backward(g3 @ w3, h1)  # g (1 - h1^2), one kernel
         dw1, db1 = _tall_tn(dz1, ax), dz1.sum(0)
-        dx = (dz1 @ w1) * (1.0 - ax * ax)
+        dx = torch.ops.aten.tanh_backward(dz1 @ w1, ax)
         e = ctx.e_dim
         oh = F.one_hot(a_prev + 1, ctx.n_emb).to(dx.dtype)
         daw = _tall_tn(oh, dx[:, e:].contiguous())
@@ -755,6 +751,7 @@ class BatchedA2C:
         if self.t == self.T:
             self.learn()
 
+    @torch.no_grad()
     def _policy(self, t):
         """Acting at window slot t: the policy on (o_t, a_{t-1}, h_t), an action per agent into act[t], the new
         recurrent states into the static _ha_new / _hc_new (reuse_acting: the mix activations into ax / h1 / mx [t],

@@ -23,7 +23,6 @@ def main():
     ap.add_argument('--eager', action='store_true', help='no HIP-graph capture of the update (BatchedA2C graph=False)')
     ap.add_argument('--act-graph', action='store_true', help='acting steps as HIP graphs (BatchedA2C act_graph=True)')
     ap.add_argument('--split-rows', type=int, default=0, help='marl.SPLIT_ROWS (rows per split-K GEMM batch)')
-    ap.add_argument('--tall-sum', default=None, help="marl.TALL_SUM ('sum' or 'gemv')")
     args = ap.parse_args()
     import torch
     from mfg_amd.factory import BatchedFactory
@@ -31,8 +30,6 @@ def main():
     import mfg_amd.marl as M
     if args.split_rows:
         M.SPLIT_ROWS = args.split_rows
-    if args.tall_sum:
-        M.TALL_SUM = args.tall_sum
     f = BatchedFactory(args.config, args.batch, seed_base=0)
     tr = BatchedA2C(f, n_steps=args.n_steps, check_cap=True, graph=not args.eager, act_graph=args.act_graph)
     tr.train(3)  # warm-up (allocations, kernels; graph=True: two eager updates, then the capture)
@@ -54,7 +51,7 @@ def main():
     out = {"what": "on-GPU A2C (BatchedA2C): act + mfg_step(packed obs, fused obs_proj) + learn every n_steps",
            "update": "eager" if args.eager else "HIP graph (captured once, replayed per update)",
            "acting": "HIP graph per window slot" if args.act_graph else "eager",
-           "split_rows": M.SPLIT_ROWS, "tall_sum": M.TALL_SUM, "config": args.config, "envs": args.batch, "agents": f.spec.n_agents, "updates": args.updates,
+           "split_rows": M.SPLIT_ROWS, "config": args.config, "envs": args.batch, "agents": f.spec.n_agents, "updates": args.updates,
            "n_steps": args.n_steps, "env_steps_per_s": round(args.batch * steps / el, 1),
            "agent_steps_per_s": round(args.batch * f.spec.n_agents * steps / el, 1),
            "ms_per_update": round(el / args.updates * 1e3, 3),

@@ -16,7 +16,6 @@ def main():
     ap.add_argument('--updates', type=int, default=3)
     ap.add_argument('--recompute', action='store_true')
     ap.add_argument('--split-rows', type=int, default=0, help='marl.SPLIT_ROWS (rows per split-K GEMM batch)')
-    ap.add_argument('--tall-sum', default=None, help="marl.TALL_SUM ('sum' or 'gemv')")
     args = ap.parse_args()
     import torch
     from torch.profiler import profile, ProfilerActivity
@@ -25,8 +24,6 @@ def main():
     import mfg_amd.marl as M
     if args.split_rows:
         M.SPLIT_ROWS = args.split_rows
-    if args.tall_sum:
-        M.TALL_SUM = args.tall_sum
     f = BatchedFactory('large8.yaml', args.batch, seed_base=0)
     tr = BatchedA2C(f, n_steps=5, check_cap=True)
     if args.recompute:
@@ -58,7 +55,7 @@ def main():
     rows.sort(reverse=True)
     tot = sum(r[0] for r in rows)
     print(f'learner update ({"recompute" if args.recompute else "saved acting pass"}), B={args.batch}, '
-          f'SPLIT_ROWS {M.SPLIT_ROWS}, TALL_SUM {M.TALL_SUM}: '
+          f'SPLIT_ROWS {M.SPLIT_ROWS}: '
           f'{tot / 1e3:.3f} ms device kernels per update')
     for us, n, k in rows[:40]:
         print(f'{us / 1e3:8.3f} ms {n:6.1f}x  {k[:120]}')
