@@ -38,6 +38,7 @@ enum {
   H_TOTAL_STEPS,   // env-steps since creation (Philox counter)
   H_N_MACHINES, H_MACHINE_BASE, H_N_MAINTS, H_MAINT_BASE,
   H_GRAPH_BUILT,   // Gamestate.floortile_graph exists (built once per env lifetime, states.py:82-87)
+  H_DIRT_TOUCH,    // step-local: this step changed a dirt table (0 in every written-back record)
   H__END
 };
 static_assert(H__END <= MFG_HDR_N, "header overflow");

@@ -836,7 +836,7 @@ __device__ void global_remove_id(const Env& e, int cell, int id) {
       case K_POD: e.pods()[slot] &= ~EW_PRESENT; break;
       case K_DROP: e.drops()[slot] &= ~EW_PRESENT; break;
       case K_DEST: e.dests()[slot] &= ~EW_PRESENT; break;
-      case K_DIRT: e.dirtpos()[slot] &= ~EW_PRESENT; break;
+      case K_DIRT: e.dirtpos()[slot] &= ~EW_PRESENT; e.hdrp[H_DIRT_TOUCH] = 1; break;
       case K_MACHINE: e.machines()[slot] &= ~EW_PRESENT; break;
       case K_MAINT: e.maints()[slot] &= ~EW_PRESENT; break;
       default: break;
@@ -1012,7 +1012,10 @@ __device__ int dirt_trigger_spawn(const Env& e, int q, double amount, int* valid
     if (k >= 0) {
       double nv = e.dirtamt()[k] + a;
       wave_sync();
-      if (e.lane == 0) e.dirtamt()[k] = nv < DIRTPILE_MAX_LOCAL ? nv : DIRTPILE_MAX_LOCAL;
+      if (e.lane == 0) {
+        e.dirtamt()[k] = nv < DIRTPILE_MAX_LOCAL ? nv : DIRTPILE_MAX_LOCAL;
+        e.hdrp[H_DIRT_TOUCH] = 1;
+      }
       wave_sync();
     } else {
       if (nd >= e.S->dirt_cap) { e.setH(H_OVERFLOW, 1); *valid = 0; return counter; }
@@ -1023,6 +1026,7 @@ __device__ int dirt_trigger_spawn(const Env& e, int q, double amount, int* valid
         e.dirtpos()[nd] = cell | EW_ALIVE | (present ? EW_PRESENT : 0);
         e.dirtid()[nd] = id;
         e.dirtamt()[nd] = a;
+        e.hdrp[H_DIRT_TOUCH] = 1;
       }
       e.setH(H_CNT_DIRT, id + 1);
       e.setH(H_N_DIRT, nd + 1);
@@ -1051,6 +1055,7 @@ __device__ void dirt_delete(const Env& e, int k) {
     wave_sync();
   }
   e.setH(H_N_DIRT, nd - 1);
+  e.setH(H_DIRT_TOUCH, 1);
   wave_sync();
 }
 
@@ -1228,7 +1233,10 @@ __device__ void do_action(const Env& e, StepOut<NW>& o, int a, int slot) {
         dirt_delete(e, k);
       } else {
         wave_sync();
-        if (e.lane == 0) e.dirtamt()[k] = na < DIRTPILE_MAX_LOCAL ? na : DIRTPILE_MAX_LOCAL;
+        if (e.lane == 0) {
+          e.dirtamt()[k] = na < DIRTPILE_MAX_LOCAL ? na : DIRTPILE_MAX_LOCAL;
+          e.hdrp[H_DIRT_TOUCH] = 1;
+        }
         wave_sync();
       }
       valid = 1;
@@ -3305,15 +3313,23 @@ __device__ __forceinline__ void rec_copy(uint8_t* dst, const uint8_t* src, int b
 #ifndef MFG_LOGIC_TRIM
 #define MFG_LOGIC_TRIM 1
 #endif
-__device__ __forceinline__ void prefix_copy(uint8_t* dst, const uint8_t* src, SpecP S, int nd, int lane) {
+// dirt = false (the write-back of a step that changed no dirt table, H_DIRT_TOUCH): the dirt slots are skipped; a
+// 16-B chunk shared with a neighbouring field goes back with its staged (unchanged) dirt bytes
+__device__ __forceinline__ void prefix_copy(uint8_t* dst, const uint8_t* src, SpecP S, int nd, int lane,
+                                            bool dirt = true) {
   auto seg = [&](int b, int end) {
     b &= ~15;
     end = (end + 15) & ~15;
     for (int i = b + 16 * lane; i < end; i += 16 * MFG_WAVE) *(uint4*)(dst + i) = *(const uint4*)(src + i);
   };
-  seg(0, S->L.o_dirt_pos + 4 * nd);
-  seg(S->L.o_dirt_id, S->L.o_dirt_id + 4 * nd);
-  seg(S->L.o_battery, S->L.o_dirt_amt + 8 * nd);
+  if (dirt) {
+    seg(0, S->L.o_dirt_pos + 4 * nd);
+    seg(S->L.o_dirt_id, S->L.o_dirt_id + 4 * nd);
+    seg(S->L.o_battery, S->L.o_dirt_amt + 8 * nd);
+  } else {
+    seg(0, S->L.o_dirt_pos);
+    seg(S->L.o_battery, S->L.o_dirt_amt);
+  }
   seg(S->L.o_pcg, S->L.o_logic);
 }
 
@@ -3375,6 +3391,7 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) k_reset(const MfgDevSpec*
     e.setH(H_OBS_INIT, 1);  // the reference renders right after every reset
   }
   e.setH(H_DONE, 0);
+  e.setH(H_DIRT_TOUCH, 0);
   wave_sync();
   rec_copy(rec, e.lds, S->L.size, e.lane);
 }
@@ -3509,13 +3526,19 @@ static __global__ void __launch_bounds__(MFG_WPB * 64) MFG_WPE_LOGIC(FULL || MAI
   // step's k_resetdone) has finished
   if (blockIdx.x == 0 && threadIdx.x < 2) S->rd_list[(size_t)(rd_slot ^ 1) * (size_t)(B + 2) + threadIdx.x] = 0;
   wave_sync();
+  // most lean steps touch no dirt pile (C5: ~6 of its ~8 KB prefix are the live piles' slots): with trim those slots
+  // go back only when the step changed one (the flag is step-local: cleared in every record written back)
+  const bool dirt_w = e.H(H_DIRT_TOUCH) != 0;
+  wave_sync();
+  e.setH(H_DIRT_TOUCH, 0);
+  wave_sync();
   if (one_pass) {
     if (e.lane < (bytes >> 4)) {
       const uint4 v = ((const uint4*)e.lds)[e.lane];
       if (v.x != orig.x || v.y != orig.y || v.z != orig.z || v.w != orig.w) ((uint4*)rec)[e.lane] = v;
     }
   } else if (trim) {
-    prefix_copy(rec, e.lds, S, nd0, e.lane);
+    prefix_copy(rec, e.lds, S, nd0, e.lane, dirt_w);
   } else {
     rec_copy(rec, e.lds, bytes, e.lane);
   }
@@ -3550,6 +3573,7 @@ k_resetdone(const MfgDevSpec* S_, uint8_t* state, long long B, int rd_slot) {
     wave_sync();
     env_reset<NW>(e, e.scratch);
     e.setH(H_DONE, 0);
+    e.setH(H_DIRT_TOUCH, 0);
     wave_sync();
     rec_copy(rec, e.lds, S->L.size, e.lane);
     wave_sync();
