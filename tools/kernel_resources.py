@@ -47,7 +47,7 @@ def main():
         rows = [r for r in unit_rows(u) if '_Z' in r['name'] and ('k_' in r['name'])]
         names = demangle([r['name'] for r in rows])
         for r, n in zip(rows, names):
-            n = re.sub(r'\(.*', '', n).replace('MfgDevSpec const*', '')
+            n = re.sub(r'\(.*', '', n.replace('(anonymous namespace)::', '')).replace('MfgDevSpec const*', '')
             print(f"| {u} | `{n}` | {r.get('sgpr')} | {r.get('vgpr')} | {r.get('sgpr_spill')} | {r.get('vgpr_spill')} "
                   f"| {r.get('scratch')} | {r.get('waves')} |")
 
