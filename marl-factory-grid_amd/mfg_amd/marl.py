@@ -326,7 +326,8 @@ def _packed_grads(idx, val, g, k):
     """obs_proj's (weight [E, k], bias [E]) gradients from packed rows idx / val [M, cap] and g [M, E]: D^T g with D
     the rows made dense (on the GPU by mfg_packed_densify, include/mfg_learn.h: one coalesced pass, no zero fill
     or scatter_add), one split-K GEMM per block of <= 512 MiB of dense rows, and the column sums of g."""
-    if not (g.is_cuda and idx.dtype == torch.uint16):
+    if not (g.is_cuda and idx.dtype == torch.uint16) or k > _DENSIFY_MAX_K:
+        # (k past the densify kernel's wave-private LDS row: the same dense rows by scatter_add on the device)
         return _packed_weight_grad(idx.long(), val, g, k).t(), g.sum(0)
     L, st = _gru_lib(), torch.cuda.current_stream(g.device).cuda_stream
     idx, val = idx.contiguous(), val.contiguous()
@@ -343,6 +344,7 @@ def _packed_grads(idx, val, g, k):
 
 
 _GRU_LIB = None
+_DENSIFY_MAX_K = 4096  # mfg_packed_densify's bound on the dense row length (include/mfg_learn.h)
 
 
 def _gru_lib():

@@ -440,7 +440,7 @@ def _rand_packed(m, cap, k, gen, fill=0.7):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('m,cap,k,e', [(5000, 32, 343, 96), (3000, 70, 1000, 96), (777, 8, 50, 20)])
+@pytest.mark.parametrize('m,cap,k,e', [(5000, 32, 343, 96), (3000, 70, 1000, 96), (777, 8, 50, 20), (600, 16, 5000, 24)])
 def test_packed_grads_match_dense(m, cap, k, e):
     """The learner's obs_proj gradients from packed rows (mfg_packed_densify, bit-exact dense rows, then the split-K
     GEMM; C3's k = 343, a wide k = 1000, cap 70 past one wave) against the dense rows' f64 GEMM and column sum."""
@@ -450,11 +450,16 @@ def test_packed_grads_match_dense(m, cap, k, e):
     g = torch.randn((m, e), generator=gen)
     d = torch.zeros((m, k), dtype=torch.float64)
     d.scatter_add_(1, idx, val.double())
-    dd = torch.full((m, k + 3), -1.0, device='cuda')  # row stride k + 3: the pad columns stay untouched
     iu, vc = idx.to(torch.uint16).cuda(), val.cuda()
-    assert M._gru_lib().mfg_packed_densify(iu.data_ptr(), vc.data_ptr(), m, cap, k, dd.data_ptr(), k + 3,
-                                           torch.cuda.current_stream().cuda_stream) == 0
-    assert torch.equal(dd[:, :k].cpu(), d.float()) and bool((dd[:, k:] == -1).all())
+    if k <= M._DENSIFY_MAX_K:
+        dd = torch.full((m, k + 3), -1.0, device='cuda')  # row stride k + 3: the pad columns stay untouched
+        assert M._gru_lib().mfg_packed_densify(iu.data_ptr(), vc.data_ptr(), m, cap, k, dd.data_ptr(), k + 3,
+                                               torch.cuda.current_stream().cuda_stream) == 0
+        assert torch.equal(dd[:, :k].cpu(), d.float()) and bool((dd[:, k:] == -1).all())
+    else:  # past the kernel's bound: refused, and _packed_grads takes the scatter_add rows instead
+        dd = torch.empty((m, k), device='cuda')
+        assert M._gru_lib().mfg_packed_densify(iu.data_ptr(), vc.data_ptr(), m, cap, k, dd.data_ptr(), k,
+                                               torch.cuda.current_stream().cuda_stream) == -1
     ref_w, ref_b = (d.t() @ g.double()).t(), g.double().sum(0)
     gw, gb = M._packed_grads(iu, vc, g.cuda(), k)
     assert gw.shape == (e, k) and gb.shape == (e,)
