@@ -39,7 +39,8 @@ int mfg_packed_project(const uint16_t* idx, const float* val, int64_t m, int cap
                        int e_dim, int k, float* out, int64_t out_row, void* stream);
 
 /* out[r] ~ Categorical(logits = logits[r][:n_act]) by inversion at u[r] in [0, 1) (the acting step's
- * Categorical(logits).sample(), base_ac.py:74-76, with the uniforms drawn by the caller) */
+ * Categorical(logits).sample(), base_ac.py:74-76, with the uniforms drawn by the caller); -1 for a row whose
+ * logits are not finite (torch.distributions would raise there) */
 int mfg_sample_categorical(const float* logits, int64_t logit_row, int n_act, const float* u, int64_t n, int32_t* out,
                            void* stream);
 

@@ -140,6 +140,10 @@ __global__ void __launch_bounds__(256) k_sample_cat(const float* __restrict__ lo
   for (int a = 1; a < n_act; a++) mx = fmaxf(mx, l[a]);
   float s = 0.0f;
   for (int a = 0; a < n_act; a++) s += expf(l[a] - mx);
+  if (!(s > 0.0f) || isinf(s)) {  // non-finite logits (NaN / inf): no distribution; -1 lets the caller report it
+    out[r] = -1;
+    return;
+  }
   const float thr = u[r] * s;
   float c = 0.0f;
   int pick = n_act - 1;  // rounding past the last bin picks the last action

@@ -914,6 +914,9 @@ class BatchedA2C:
         """One A2C update on the window (base_ac.py:200-225), then slide: o_T becomes o_0."""
         if self.check_cap:
             self.pobs.check()
+            if self.gen is None and self.dev.type == 'cuda' and bool((self.act < 0).any()):
+                # mfg_sample_categorical marks rows with non-finite logits -1 (the engine took them as crash actions)
+                raise RuntimeError('BatchedA2C: non-finite policy logits in this window (training diverged)')
         # episode and reward counters once per window (two reductions instead of two per step)
         self.episodes += self.done.sum()
         self.reward_sum += self.rew.sum()

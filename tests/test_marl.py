@@ -511,6 +511,12 @@ def test_sample_categorical_kernel_distribution():
     assert L.mfg_sample_categorical(lg.data_ptr(), 5, 5, u.data_ptr(), n, out.data_ptr(), st) == 0
     freq = torch.bincount(out.long(), minlength=5).double().cpu() / n
     assert float((freq - p).abs().max()) < 3e-3, (freq, p)
+    # non-finite logits: no distribution, the row is marked -1 (BatchedA2C.learn raises on it)
+    bad = torch.tensor([[0.0, float('nan'), 1.0], [float('inf'), 0.0, 0.0], [0.0, 1.0, 2.0]], device='cuda')
+    u3 = torch.full((3,), 0.5, device='cuda')
+    o3 = torch.empty(3, dtype=torch.int32, device='cuda')
+    assert L.mfg_sample_categorical(bad.data_ptr(), 3, 3, u3.data_ptr(), 3, o3.data_ptr(), st) == 0
+    assert o3.cpu().tolist()[:2] == [-1, -1] and 0 <= int(o3[2]) < 3
 
 
 def test_saved_mix_backward_matches_autograd():
