@@ -29,7 +29,7 @@ HDR = {k: i for i, k in enumerate([
     'n_dirt', 'n_dests', 'item_base', 'pod_base', 'drop_base', 'dest_base', 'bat_base', 'arrival', 'done',
     'overflow', 'cnt_agent', 'cnt_battery', 'cnt_pod', 'cnt_drop', 'cnt_item', 'cnt_dirt', 'cnt_dest',
     'cnt_machine', 'cnt_maint', 'cnt_gp', 'total_steps', 'n_machines', 'machine_base', 'n_maints', 'maint_base',
-    'graph_built'])}
+    'graph_built', 'dirt_touch'])}
 
 _lib = None
 
