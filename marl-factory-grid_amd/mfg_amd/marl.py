@@ -636,6 +636,14 @@ class BatchedA2C:
     synchronisation inside ``step``;
     ``learn`` syncs once when ``check_cap`` is set (truncated packed rows raise).
 
+    ``reuse_acting=True`` (the default on the GPU, without the agent embedding): the weights are fixed over a window, so
+    the acting steps' forward is the learner's forward of entries 0..T-1. Acting runs the mix and both GRUs itself
+    (``mfg_gru_fwd_step``) and keeps every activation in entry-major window buffers; the learner evaluates the heads
+    and the loss with grad and runs the mix / GRU backward on the stored activations (``_MixSaved``,
+    ``_GRUWindowSavedT``), plus one no-grad critic step for the bootstrap entry T. ``_loss_recompute`` is the
+    reference learner's full-window recompute (pinned equal). Sampling on the GPU is ``mfg_sample_categorical`` (a
+    row with non-finite logits is marked -1 and ``learn`` raises when ``check_cap`` is set).
+
     ``graph=True``: the update (loss, backward, gradient clipping, RMSprop step and the window slide, ~1,300 launches)
     is captured once as a HIP graph after two eager warm-up updates on a side stream and replayed from then on (one
     launch per update); the optimizer then keeps its step counters on the device (``capturable``).
