@@ -249,3 +249,17 @@ def test_large_qquad_with_its_doors_compiles():
     from mfg_amd.spec import compile_spec
     s = compile_spec('qquad_doors.yaml')
     assert s.c.n_doors == 65 and s.c.has_doors
+
+
+def test_record_header_slots_match_device_enum():
+    """engine.HDR (the host decoder's header slot names) follows the device enum in csrc/mfg_device.h slot for slot,
+    so RecordView reads the slot the kernels write (H_STEP .. H_DIRT_TOUCH); and both fit MFG_HDR_N."""
+    import re
+    from pathlib import Path
+    from mfg_amd.engine import HDR, HDR_N
+    src = (Path(__file__).resolve().parents[1] / 'marl-factory-grid_amd' / 'csrc' / 'mfg_device.h').read_text()
+    body = src[src.index('H_STEP = 0'):src.index('H__END')]
+    body = re.sub(r'//[^\n]*', '', body)
+    names = [n.strip()[2:].lower() for n in body.replace('= 0', '').split(',') if n.strip()]
+    assert names == list(HDR), (names, list(HDR))
+    assert len(names) <= HDR_N == int(re.search(r'#define MFG_HDR_N (\d+)', src).group(1))
